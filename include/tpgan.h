@@ -1,0 +1,132 @@
+/*
+ * tpgan.h — C-ABI of libtpgan_hip.so, the MI355X (gfx950) kernels of the TP-GAN
+ * generator/discriminator hot path.
+ *
+ * The reference (PandaKenWei/TP-GAN) has no FFI: its hot path is torch.nn layers called
+ * from Python.  Each entry point below replaces one aten call the
+ * reference's layer factories make; the Python host side (tp-gan_amd/tpgan_lib.py) binds
+ * them with ctypes and keeps the reference's module/class/state_dict API on top.
+ *
+ *   tpg_conv2d_fwd          nn.Conv2d / nn.ConvTranspose2d forward + bias + activation
+ *                           (+ residual add) — ModificationLayer.py:54-123 conv(),
+ *                           :158-202 deconv(), :298-302 ResidualBlock.forward,
+ *                           and the ReflectionPad2d of :83-96 (pad_mode = reflect);
+ *                           also Linear (fc1, D_and_G_model.py:212) as a full-kernel conv.
+ *   tpg_conv2d_bwd_data     the input gradient of the same op (aten convolution_backward)
+ *   tpg_conv2d_bwd_filter   the weight gradient (accumulated into fp32)
+ *   tpg_act_bwd             activation' mask (LeakyReLU 0.01 / ReLU, from the saved output)
+ *                           + bias gradient
+ *   tpg_copy4d              dtype/layout conversion and torch.cat into a channel slice
+ *                           (D_and_G_model.py:100,102,104,293,298,307,311,312,317,318,323,324)
+ *   tpg_local_fuse_fwd/bwd  LocalFuser (D_and_G_model.py:132-159): zero-pad + max over 4 parts
+ *   tpg_maxout2_fwd/bwd     fc2 maxout, MaxPool1d(2,2) (D_and_G_model.py:214,290)
+ *   tpg_adam                the optimizer update (UtilityMethods.py:14-41 getOptimizer 'Adam')
+ *
+ * Conventions
+ *   - Every tensor is described by tpg_tensor: a device pointer, a dtype and the element
+ *     strides of its LOGICAL NCHW view (n, c, h, w).  Kernels are fastest on
+ *     channels-last (NHWC) tensors whose pixel stride is a multiple of 8 elements, which
+ *     is what the host side allocates; any other strides are accepted on slower paths.
+ *   - Weights are the fp32 master parameters, logical [a][b][kh][kw]
+ *     (Conv2d: a = out, b = in; ConvTranspose2d: a = in, b = out), any strides.
+ *   - Ownership: every pointer is caller-owned device memory; the library never
+ *     allocates or frees and keeps no state besides a thread-local error string.
+ *   - Work space: query tpg_conv2d_workspace(); pass at least that many bytes.
+ *   - Streams: every call enqueues on the given stream only, never synchronises, and is
+ *     therefore legal inside hipStreamBeginCapture (hipGraph) regions.
+ *   - Errors: 0 on success, negative for a bad descriptor / unsupported shape, positive
+ *     hipError_t for a launch failure; tpg_last_error() returns the message.
+ */
+#ifndef TPGAN_H
+#define TPGAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* tpg_stream_t; /* hipStream_t */
+
+enum { TPG_F32 = 0, TPG_BF16 = 1 };
+enum { TPG_ACT_NONE = 0, TPG_ACT_RELU = 1, TPG_ACT_LEAKY = 2 };
+enum { TPG_PAD_ZERO = 0, TPG_PAD_REFLECT = 1 };
+enum { TPG_OP_FWD = 0, TPG_OP_BWD_DATA = 1, TPG_OP_BWD_FILTER = 2 };
+
+typedef struct tpg_tensor {
+  void* data;
+  int32_t dtype;      /* TPG_F32 / TPG_BF16 */
+  int32_t reserved;
+  int64_t stride[4];  /* element strides of the logical (n, c, h, w) view */
+} tpg_tensor;
+
+typedef struct tpg_conv_desc {
+  int32_t n;                      /* batch */
+  int32_t in_c, in_h, in_w;       /* input  (logical NCHW) */
+  int32_t out_c, out_h, out_w;    /* output (logical NCHW) */
+  int32_t kh, kw;                 /* kernel */
+  int32_t stride_h, stride_w;
+  int32_t pad_t, pad_b, pad_l, pad_r;
+  int32_t pad_mode;               /* TPG_PAD_*; reflect only for transposed == 0 */
+  int32_t transposed;             /* 0: Conv2d, 1: ConvTranspose2d (output_padding = out - natural) */
+  int32_t dtype;                  /* activation / arithmetic dtype, TPG_F32 or TPG_BF16 */
+  int32_t act;                    /* TPG_ACT_* applied after bias (+ residual) */
+  float slope;                    /* LeakyReLU negative slope */
+  float res_scale;                /* ResidualBlock scaling_factor (ModificationLayer.py:300) */
+  int32_t ksplit;                 /* 0 = automatic split-K, >=1 forces */
+  int32_t reserved;
+} tpg_conv_desc;
+
+/* Workspace bytes needed by op (TPG_OP_*) for this descriptor. */
+size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op);
+
+/* y = act(conv(x, w) + bias [+ res_scale * residual]).  residual.data may be NULL; bias may be NULL. */
+int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, const float* bias,
+                       tpg_tensor residual, tpg_tensor y, void* ws, size_t ws_bytes, tpg_stream_t stream);
+
+/* dx = dconv/dx applied to g (g is the already-masked output gradient, see tpg_act_bwd). */
+int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx,
+                            void* ws, size_t ws_bytes, tpg_stream_t stream);
+
+/* dw += dconv/dw (fp32, dw strides given by the tensor; dw.dtype must be TPG_F32). */
+int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw,
+                              void* ws, size_t ws_bytes, tpg_stream_t stream);
+
+/* g = gy * act'(y) over logical [n, c, h, w]; dbias[c] += sum g (dbias may be NULL). */
+int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
+                    tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, tpg_stream_t stream);
+
+/* out = in over logical [n, c, h, w] with dtype conversion; in and out may have any strides
+ * (an out view offset into a wider channels-last buffer implements torch.cat). */
+int32_t tpg_copy4d(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor in, tpg_tensor out,
+                   tpg_stream_t stream);
+
+/* LocalFuser: part k (logical [n, c, ph[k], pw[k]]) is placed at (top[k], left[k]) of an
+ * out_h x out_w zero canvas; y = max over k, argmax = first k attaining it (uint8, NHWC order). */
+int32_t tpg_local_fuse_fwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, const tpg_tensor* parts,
+                           const int32_t* ph, const int32_t* pw, const int32_t* top, const int32_t* left,
+                           tpg_tensor y, uint8_t* argmax, tpg_stream_t stream);
+int32_t tpg_local_fuse_bwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, tpg_tensor gy,
+                           const uint8_t* argmax, const tpg_tensor* dparts, const int32_t* ph,
+                           const int32_t* pw, const int32_t* top, const int32_t* left, tpg_stream_t stream);
+
+/* fc2 maxout: y[b, j] = max(x[b, 2j], x[b, 2j+1]) (first index wins ties), x logical [b, 2m]. */
+int32_t tpg_maxout2_fwd(int32_t b, int32_t m, tpg_tensor x, tpg_tensor y, uint8_t* argmax, tpg_stream_t stream);
+int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argmax, tpg_tensor dx,
+                        tpg_stream_t stream);
+
+/* In-place Adam (torch.optim.Adam semantics, L2 weight_decay added to the gradient) on a
+ * flat fp32 buffer; step is the 1-based step count after increment. grad_scale multiplies g. */
+int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                 float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
+                 float grad_scale, tpg_stream_t stream);
+
+/* Library version string and the thread-local message of the last failed call. */
+const char* tpg_version(void);
+const char* tpg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPGAN_H */

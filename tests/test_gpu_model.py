@@ -1,0 +1,92 @@
+"""End-to-end GPU parity: the product's Generator + Discriminator (fp32 MFMA path) on
+the reference's own B=2 golden run (tests/golden/e2e_golden.npz: outputs of
+D_and_G_model.Generator/Discriminator with R1-R3 and deterministic weights, float64),
+including per-parameter gradient summaries for all 348 parameter tensors."""
+import numpy as np
+import pytest
+import torch
+
+from _cases import golden, load_det, rel
+
+pytestmark = pytest.mark.gpu
+
+G_OUT = ["I128_fake", "encoder_predict", "fused_local_fake", "le_fake", "re_fake", "nose_fake", "mouth_fake",
+         "fused_local_real"]
+INS = ["I128", "left_eye", "right_eye", "nose", "mouth", "z"]
+
+
+@pytest.fixture(scope="module")
+def e2e(gpu):
+    import D_and_G_model as DG
+    E = golden("e2e_golden.npz")
+    G = DG.Generator(64, 347, use_batchnorm=False)
+    D = DG.Discriminator()
+    load_det(G, "G/", torch.float32)
+    load_det(D, "D/", torch.float32)
+    G, D = G.to(gpu), D.to(gpu)
+    ins = {k: torch.from_numpy(E["in:" + k]).float().to(gpu).requires_grad_(True) for k in INS}
+    outs = G(ins["I128"], ins["left_eye"], ins["right_eye"], ins["nose"], ins["mouth"], ins["z"], False)
+    loss = 0
+    from oracle.det_init import det_uniform
+    for name, o in zip(G_OUT, outs):
+        if name == "fused_local_real":
+            continue
+        pr = torch.from_numpy(det_uniform("proj/e2e/" + name, o.numel())).reshape(o.shape).float().to(gpu)
+        loss = loss + (o * pr).sum()
+    d_fake = D(outs[0])
+    pr = torch.from_numpy(det_uniform("proj/e2e/d_fake", d_fake.numel())).reshape(d_fake.shape).float().to(gpu)
+    loss = loss + (d_fake * pr).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    return E, G, D, ins, outs, d_fake
+
+
+def test_generator_outputs(e2e):
+    E, G, D, ins, outs, d_fake = e2e
+    for name, o in zip(G_OUT, outs):
+        ref = E["out:" + name]
+        assert tuple(o.shape) == ref.shape, name
+        assert rel(o.detach().cpu(), ref) < 1e-3, name
+    assert rel(d_fake.detach().cpu(), E["out:d_fake"]) < 1e-3
+
+
+def test_input_grads(e2e):
+    E, G, D, ins, outs, d_fake = e2e
+    for k in INS:
+        if "din:" + k in E.files:
+            assert rel(ins[k].grad.cpu(), E["din:" + k]) < 1e-3, k
+
+
+def _check_gsum(E, prefix, model):
+    from oracle.det_init import det_uniform
+    allg, allr = [], []
+    worst = 0.0
+    for k, p in model.named_parameters():
+        ref = E["gsum:%s/%s" % (prefix, k)]
+        g = p.grad.detach().double().reshape(-1).cpu().numpy()
+        u = det_uniform("sample/%s/%s" % (prefix, k), 16)
+        idx = np.floor((u + 1.0) * 0.5 * g.size).astype(np.int64).clip(0, g.size - 1)
+        norm = np.sqrt((g * g).sum())
+        worst = max(worst, abs(norm - ref[0]) / max(ref[0], 1e-30))
+        allg.append(g[idx])
+        allr.append(ref[2:])
+    # per-tensor norm within 1e-2, concatenated samples within 1e-3
+    assert worst < 1e-2, worst
+    assert rel(np.concatenate(allg), np.concatenate(allr)) < 1e-3
+
+
+def test_generator_param_grads(e2e):
+    E, G, D, ins, outs, d_fake = e2e
+    _check_gsum(E, "G", G)
+
+
+def test_discriminator_param_grads(e2e):
+    E, G, D, ins, outs, d_fake = e2e
+    _check_gsum(E, "D", D)
+
+
+def test_discriminator_real(e2e, gpu):
+    E, G, D, ins, outs, d_fake = e2e
+    with torch.no_grad():
+        d = D(ins["I128"].detach())
+    assert rel(d.cpu(), E["out:d_real"]) < 1e-3

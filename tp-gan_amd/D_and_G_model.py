@@ -1,0 +1,266 @@
+"""TP-GAN generator and discriminator (reference D_and_G_model.py), MI355X-native.
+
+Module names, constructor signatures, forward signatures / return tuples and state_dict
+keys are the reference's (`/root/reference/D_and_G_model.py`).  Architecture = reference
++ repairs R1-R3; R3 sizes the 128-px fusion for the 75 channels the
+forward actually concatenates (:323): dim128 = 75, enhance_features_128 = 206 channels,
+conv5 input 206.
+
+Every Conv2d / ConvTranspose2d / Linear / concat / LocalFuser max / maxout runs on the
+HIP kernels of libtpgan_hip.so (tpgan_ops); there is no CPU path.
+"""
+import torch
+import torch.nn as nn
+
+import tpgan_ops
+from ModificationLayer import *  # noqa: F401,F403  (conv, deconv, sequential, ResidualBlock, ...)
+from ModificationLayer import ResidualBlock, conv, deconv, sequential
+from UtilityMethods import elementwise_multiply_and_cast_to_int as EMaC2I
+
+
+class LocalPathway(nn.Module):
+    """U-Net over one landmark patch (D_and_G_model.py:18-110): encoder 64/128/256/512,
+    transposed-conv decoder with skip concats, 1x1 conv to RGB."""
+
+    def __init__(self, use_batchnorm=True, feature_layer_dim=64, FM_multiplier=1.0):
+        super(LocalPathway, self).__init__()
+        n_FM_encoder = EMaC2I([64, 128, 256, 512], FM_multiplier)
+        n_FM_decoder = EMaC2I([256, 128], FM_multiplier)
+        L = nn.LeakyReLU
+        self.conv0 = sequential(conv(3, n_FM_encoder[0], 3, 1, 1, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(n_FM_encoder[0], activation=L()))
+        self.conv1 = sequential(conv(n_FM_encoder[0], n_FM_encoder[1], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(n_FM_encoder[1], activation=L()))
+        self.conv2 = sequential(conv(n_FM_encoder[1], n_FM_encoder[2], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(n_FM_encoder[2], activation=L()))
+        self.conv3 = sequential(conv(n_FM_encoder[2], n_FM_encoder[3], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(n_FM_encoder[3], activation=L()))
+        self.deconv0 = deconv(n_FM_encoder[3], n_FM_decoder[0], 3, 2, 1, 1, "kaiming", nn.ReLU(), use_batchnorm)
+        self.after_select0 = sequential(
+            conv(n_FM_decoder[0] + self.conv2.out_channels, n_FM_decoder[0], 3, 1, 1, "kaiming", L(), use_batchnorm),
+            ResidualBlock(n_FM_decoder[0], activation=L()))
+        self.deconv1 = deconv(self.after_select0.out_channels, n_FM_decoder[1], 3, 2, 1, 1, "kaiming", nn.ReLU(),
+                              use_batchnorm)
+        self.after_select1 = sequential(
+            conv(n_FM_decoder[1] + self.conv1.out_channels, n_FM_decoder[1], 3, 1, 1, "kaiming", L(), use_batchnorm),
+            ResidualBlock(n_FM_decoder[1], activation=L()))
+        self.deconv2 = deconv(self.after_select1.out_channels, feature_layer_dim, 3, 2, 1, 1, "kaiming", nn.ReLU(),
+                              use_batchnorm)
+        self.after_select2 = sequential(
+            conv(feature_layer_dim + self.conv0.out_channels, feature_layer_dim, 3, 1, 1, "kaiming", L(),
+                 use_batchnorm),
+            ResidualBlock(feature_layer_dim, activation=L()))
+        self.local_img = conv(feature_layer_dim, 3, 1, 1, 0, None, None, False)
+
+    def forward(self, x):
+        conv0 = self.conv0(x)
+        conv1 = self.conv1(conv0)
+        conv2 = self.conv2(conv1)
+        conv3 = self.conv3(conv2)
+        deconv0 = self.deconv0(conv3)
+        after_select0 = self.after_select0(tpgan_ops.cat([deconv0, conv2]))
+        deconv1 = self.deconv1(after_select0)
+        after_select1 = self.after_select1(tpgan_ops.cat([deconv1, conv1]))
+        deconv2 = self.deconv2(after_select1)
+        after_select2 = self.after_select2(tpgan_ops.cat([deconv2, conv0]))
+        local_img = self.local_img(after_select2)
+        assert local_img.shape == x.shape, "{} {}".format(local_img.shape, x.shape)
+        return local_img, deconv2
+
+
+class LocalFuser(nn.Module):
+    """Zero-pad the four parts onto a 128x128 canvas and take the element-wise max
+    (D_and_G_model.py:112-159).  Placements (top, left) follow the reference's pad
+    arithmetic (:154-157); ties resolve to the first part, as torch.max does."""
+
+    EYE_WIDTH, EYE_HEIGHT = 40, 40
+    NOSE_WIDTH, NOSE_HEIGHT = 40, 32
+    MOUTH_WIDTH, MOUTH_HEIGHT = 48, 32
+    IMG_SIZE = 128
+    # (top, left) of left eye, right eye, nose, mouth
+    TOPS = (40 - 20 - 1, 39 - 20 - 1, 64 - 16 - 1, 89 - 16 - 1)
+    LEFTS = (39 - 20 - 1, 86 - 20 - 1, 64 - 20 - 1, 65 - 24 - 1)
+    SIZES = ((40, 40), (40, 40), (32, 40), (32, 48))
+
+    def __init__(self):
+        super(LocalFuser, self).__init__()
+
+    def forward(self, f_left_eye, f_right_eye, f_nose, f_mouth):
+        parts = (f_left_eye, f_right_eye, f_nose, f_mouth)
+        for p, (h, w) in zip(parts, self.SIZES):
+            if tuple(p.shape[2:]) != (h, w):
+                raise RuntimeError("LocalFuser expects part of spatial size %dx%d, got %s" % (h, w, tuple(p.shape)))
+        return tpgan_ops.local_fuse(parts, (self.IMG_SIZE, self.IMG_SIZE), self.TOPS, self.LEFTS)
+
+
+class GlobalPathway(nn.Module):
+    """Global encoder-decoder over the 128x128 face (D_and_G_model.py:161-329), R3 applied."""
+
+    def __init__(self, zdim, local_feature_layer_dim=64, use_batchnorm=True, use_residual_block=True,
+                 scaling_factor=1.0, FM_multiplier=1.0):
+        super(GlobalPathway, self).__init__()
+        n_FM_encoder = EMaC2I([64, 64, 128, 256, 512], FM_multiplier)
+        n_FM_decoder = EMaC2I([64, 32, 16, 8], FM_multiplier)
+        n_FM_decoder_enhance_features = EMaC2I([512, 256, 128, 64], FM_multiplier)
+        n_FM_decoder_conv = EMaC2I([64, 32], FM_multiplier)
+        L = nn.LeakyReLU
+        self.zdim = zdim
+        self.use_residual_block = use_residual_block
+        sf = scaling_factor
+        self.conv0 = sequential(conv(3, n_FM_encoder[0], 7, 1, 3, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(64, 64, 7, 1, 3, "kaiming", L(1e-2), scaling_factor=sf))
+        self.conv1 = sequential(conv(n_FM_encoder[1], n_FM_encoder[1], 5, 2, 2, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(64, 64, 5, 1, 2, "kaiming", L(1e-2), scaling_factor=sf))
+        self.conv2 = sequential(conv(n_FM_encoder[1], n_FM_encoder[2], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(128, 128, 3, 1, 1, "kaiming", L(1e-2), scaling_factor=sf))
+        self.conv3 = sequential(conv(n_FM_encoder[2], n_FM_encoder[3], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
+                                ResidualBlock(256, 256, 3, 1, 1, "kaiming", L(1e-2), is_bottleneck=False,
+                                              scaling_factor=sf))
+        self.conv4 = sequential(conv(n_FM_encoder[3], n_FM_encoder[4], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
+                                *[ResidualBlock(512, 512, 3, 1, 1, "kaiming", L(1e-2), is_bottleneck=False,
+                                                scaling_factor=sf) for i in range(4)])
+        self.fc1 = nn.Linear(n_FM_encoder[4] * 8 * 8, 512)
+        self.fc2 = nn.MaxPool1d(2, 2, 0)
+        self.deconv_8 = deconv(256 + self.zdim, n_FM_decoder[0], 8, 1, 0, 0, "kaiming", nn.ReLU(), use_batchnorm)
+        self.deconv_32 = deconv(n_FM_decoder[0], n_FM_decoder[1], 3, 4, 0, 1, "kaiming", nn.ReLU(), use_batchnorm)
+        self.deconv_64 = deconv(n_FM_decoder[1], n_FM_decoder[2], 3, 2, 1, 1, "kaiming", nn.ReLU(), use_batchnorm)
+        self.deconv_128 = deconv(n_FM_decoder[2], n_FM_decoder[3], 3, 2, 1, 1, "kaiming", nn.ReLU(), use_batchnorm)
+        dim8 = self.deconv_8.out_channels + self.conv4.out_channels
+        self.add_conv_and_deconv_8 = ResidualBlock(dim8, dim8, 2, 1, padding=[1, 0, 1, 0], activation=L())
+        self.enhance_features_8 = sequential(
+            *[ResidualBlock(dim8, dim8, 2, 1, padding=[1, 0, 1, 0], activation=L()) for i in range(2)])
+        self.upsample_16 = deconv(self.enhance_features_8.out_channels, n_FM_decoder_enhance_features[0], 3, 2, 1, 1,
+                                  "kaiming", nn.ReLU(), use_batchnorm)
+        dim16 = self.conv3.out_channels
+        self.add_conv_and_deconv_16 = ResidualBlock(dim16, activation=L())
+        self.enhance_features_16 = sequential(
+            *[ResidualBlock(self.upsample_16.out_channels + self.add_conv_and_deconv_16.out_channels, activation=L())
+              for i in range(2)])
+        self.upsample_32 = deconv(self.enhance_features_16.out_channels, n_FM_decoder_enhance_features[1], 3, 2, 1, 1,
+                                  "kaiming", nn.ReLU(), use_batchnorm)
+        dim32 = self.conv2.out_channels + self.deconv_32.out_channels
+        self.add_conv_and_deconv_32 = ResidualBlock(dim32, activation=L())
+        self.enhance_features_32 = sequential(
+            *[ResidualBlock(self.upsample_32.out_channels + self.add_conv_and_deconv_32.out_channels, activation=L())
+              for i in range(2)])
+        self.upsample_64 = deconv(self.enhance_features_32.out_channels, n_FM_decoder_enhance_features[2], 3, 2, 1, 1,
+                                  "kaiming", nn.ReLU(), use_batchnorm)
+        dim64 = self.conv1.out_channels + self.deconv_64.out_channels
+        self.add_conv_and_deconv_64 = ResidualBlock(dim64, kernel_size=5, activation=L())
+        self.enhance_features_64 = sequential(
+            *[ResidualBlock(self.upsample_64.out_channels + self.add_conv_and_deconv_64.out_channels, activation=L())
+              for i in range(2)])
+        self.upsample_128 = deconv(self.enhance_features_64.out_channels, n_FM_decoder_enhance_features[3], 3, 2, 1,
+                                   1, "kaiming", nn.ReLU(), use_batchnorm)
+        # R3: the forward concatenates [deconv_128, conv0, I128] = 8 + 64 + 3 channels (:323)
+        dim128 = self.deconv_128.out_channels + self.conv0.out_channels + 3
+        self.add_conv_and_deconv_128 = ResidualBlock(dim128, kernel_size=7, activation=L())
+        self.enhance_features_128 = sequential(
+            *[ResidualBlock(self.upsample_128.out_channels + self.add_conv_and_deconv_128.out_channels +
+                            local_feature_layer_dim + 3, kernel_size=5, activation=L())])
+        self.conv5 = sequential(
+            conv(self.enhance_features_128.out_channels, n_FM_decoder_conv[0], 5, 1, 2, "kaiming", L(),
+                 use_batchnorm),
+            ResidualBlock(n_FM_decoder_conv[0], kernel_size=3, activation=L()))
+        self.conv6 = conv(n_FM_decoder_conv[0], n_FM_decoder_conv[1], 3, 1, 1, "kaiming", L(), use_batchnorm)
+        self.decoded_img128 = conv(n_FM_decoder_conv[1], 3, 3, 1, 1, None, activation=None)
+
+    def forward(self, I128, local_fake_image, local_feature, z):
+        cat = tpgan_ops.cat
+        conv0 = self.conv0(I128)
+        conv1 = self.conv1(conv0)
+        conv2 = self.conv2(conv1)
+        conv3 = self.conv3(conv2)
+        conv4 = self.conv4(conv3)
+        B = conv4.shape[0]
+        # fc1 on the NCHW flattening of conv4 (:289) = an 8x8 full-kernel conv on the NHWC map
+        fc1 = tpgan_ops.linear(conv4, self.fc1.weight, self.fc1.bias)
+        fc2 = tpgan_ops.maxout2(fc1)  # self.fc2 = MaxPool1d(2, 2) on view(B, -1, 2) (:290)
+        deconv_8 = self.deconv_8(cat([fc2.view(B, -1, 1, 1), z.view(B, -1, 1, 1)]))
+        deconv_32 = self.deconv_32(deconv_8)
+        deconv_64 = self.deconv_64(deconv_32)
+        deconv_128 = self.deconv_128(deconv_64)
+        add_conv_and_deconv_8 = self.add_conv_and_deconv_8(cat([deconv_8, conv4]))
+        enhance_features_8 = self.enhance_features_8(add_conv_and_deconv_8)
+        assert enhance_features_8.shape[2] == 8
+        upsample_16 = self.upsample_16(enhance_features_8)
+        add_conv_and_deconv_16 = self.add_conv_and_deconv_16(conv3)
+        enhance_features_16 = self.enhance_features_16(cat([upsample_16, add_conv_and_deconv_16]))
+        assert enhance_features_16.shape[2] == 16
+        upsample_32 = self.upsample_32(enhance_features_16)
+        add_conv_and_deconv_32 = self.add_conv_and_deconv_32(cat([deconv_32, conv2]))
+        enhance_features_32 = self.enhance_features_32(cat([upsample_32, add_conv_and_deconv_32]))
+        upsample_64 = self.upsample_64(enhance_features_32)
+        add_conv_and_deconv_64 = self.add_conv_and_deconv_64(cat([deconv_64, conv1]))
+        enhance_features_64 = self.enhance_features_64(cat([upsample_64, add_conv_and_deconv_64]))
+        upsample_128 = self.upsample_128(enhance_features_64)
+        add_conv_and_deconv_128 = self.add_conv_and_deconv_128(cat([deconv_128, conv0, I128]))
+        enhance_features_128 = self.enhance_features_128(
+            cat([upsample_128, add_conv_and_deconv_128, local_feature, local_fake_image]))
+        conv5 = self.conv5(enhance_features_128)
+        conv6 = self.conv6(conv5)
+        decoded_img128 = self.decoded_img128(conv6)
+        return decoded_img128, fc2
+
+
+class FeaturePredict(nn.Module):
+    """Dropout(0.3) + Linear(256 -> num_classes) on the maxout features (:331-348)."""
+
+    def __init__(self, num_classes, global_feature_layer_dim=256, dropout=0.3):
+        super(FeaturePredict, self).__init__()
+        self.dropout = nn.Dropout(p=dropout)
+        self.fc = nn.Linear(global_feature_layer_dim, num_classes)
+
+    def forward(self, x, use_dropout):
+        if use_dropout:
+            x = self.dropout(x)
+        return tpgan_ops.linear(x, self.fc.weight, self.fc.bias)
+
+
+class Generator(nn.Module):
+    """Four LocalPathways, three LocalFuser calls, the GlobalPathway and FeaturePredict;
+    forward returns the reference's 8-tuple (D_and_G_model.py:350-407)."""
+
+    def __init__(self, zdim, num_classes, use_batchnorm=True, use_residual_block=True):
+        super(Generator, self).__init__()
+        self.local_pathway_left_eye = LocalPathway(use_batchnorm=use_batchnorm)
+        self.local_pathway_right_eye = LocalPathway(use_batchnorm=use_batchnorm)
+        self.local_pathway_nose = LocalPathway(use_batchnorm=use_batchnorm)
+        self.local_pathway_mouth = LocalPathway(use_batchnorm=use_batchnorm)
+        self.global_pathway = GlobalPathway(zdim, use_batchnorm=use_batchnorm, use_residual_block=use_residual_block)
+        self.local_fuser = LocalFuser()
+        self.feature_predict = FeaturePredict(num_classes)
+
+    def forward(self, I128, left_eye, right_eye, nose, mouth, z, use_dropout):
+        left_eye_fake_image, left_eye_fake_feature = self.local_pathway_left_eye(left_eye)
+        right_eye_fake_image, right_eye_fake_feature = self.local_pathway_right_eye(right_eye)
+        nose_fake_image, nose_fake_feature = self.local_pathway_nose(nose)
+        mouth_fake_image, mouth_fake_feature = self.local_pathway_mouth(mouth)
+        fused_local_feature = self.local_fuser(left_eye_fake_feature, right_eye_fake_feature, nose_fake_feature,
+                                               mouth_fake_feature)
+        fused_local_fake_image = self.local_fuser(left_eye_fake_image, right_eye_fake_image, nose_fake_image,
+                                                  mouth_fake_image)
+        fused_local_origin_4_part = self.local_fuser(left_eye, right_eye, nose, mouth)
+        I128_fake, encoder_feature = self.global_pathway(I128, fused_local_fake_image, fused_local_feature, z)
+        encoder_predict = self.feature_predict(encoder_feature, use_dropout)
+        return (I128_fake, encoder_predict, fused_local_fake_image, left_eye_fake_image, right_eye_fake_image,
+                nose_fake_image, mouth_fake_image, fused_local_origin_4_part)
+
+
+class Discriminator(nn.Module):
+    """5x [3x3 s2 conv + LeakyReLU], ResidualBlocks after stages 4 and 5, 3x3 conv to one
+    channel: a B x 1 x H/32 x W/32 patch map (D_and_G_model.py:409-435)."""
+
+    def __init__(self, use_batchnorm=False, FM_multiplier=1.0):
+        super(Discriminator, self).__init__()
+        layers = []
+        n_Fmap = EMaC2I([3, 64, 128, 256, 512, 512], FM_multiplier)
+        for i in range(len(n_Fmap) - 1):
+            layers.append(conv(n_Fmap[i], n_Fmap[i + 1], 3, 2, 1, "kaiming", nn.LeakyReLU(1e-2), use_batchnorm))
+            if i >= 3:
+                layers.append(ResidualBlock(n_Fmap[i + 1], activation=nn.LeakyReLU()))
+        layers.append(conv(n_Fmap[-1], 1, kernel_size=3, stride=1, padding=1, init=None, activation=None))
+        self.model = sequential(*layers)
+
+    def forward(self, x):
+        return self.model(x)

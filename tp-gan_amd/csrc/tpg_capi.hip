@@ -1,0 +1,545 @@
+// C-ABI of libtpgan_hip.so (include/tpgan.h): turns a tpg_conv_desc into implicit-GEMM
+// problems (tpg_igemm.hip) and weight-gradient problems (tpg_wgrad.hip).
+//
+//  op          Conv2d                                  ConvTranspose2d
+//  forward     direct form: rows = output pixels,      sub-pixel form: one launch per output
+//              A = x gathered at oy*s + r - pad        parity class, taps that reach it
+//  bwd_data    sub-pixel form over the input grid,     direct form over the input grid,
+//              A = g                                   A = g gathered at iy*s + r - pad
+//  bwd_filter  P = g (output grid), Q = x gathered     P = x (input grid), Q = g gathered
+//
+// A full-kernel conv (Linear fc1 as a 8x8 conv on an 8x8 map) and a transposed conv of a
+// 1x1 map (deconv_8) become plain GEMMs over flattened (y, x, c) channels when the
+// tensors are dense NHWC ("composite" channels).
+#include "tpg_internal.h"
+#include "../../include/tpgan.h"
+#include <stdarg.h>
+#include <string.h>
+#include <stdlib.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+extern "C" int32_t tpg_act_bwd_impl(int32_t, int32_t, int32_t, int32_t, int32_t, float, tpg_tensor, tpg_tensor,
+                                     tpg_tensor, float*, hipStream_t);
+extern "C" int32_t tpg_copy4d_impl(int32_t, int32_t, int32_t, int32_t, tpg_tensor, tpg_tensor, hipStream_t);
+extern "C" int32_t tpg_fuse_fwd_impl(int32_t, int32_t, int32_t, int32_t, const tpg_tensor*, const int32_t*,
+                                      const int32_t*, const int32_t*, const int32_t*, tpg_tensor, uint8_t*, hipStream_t);
+extern "C" int32_t tpg_fuse_bwd_impl(int32_t, int32_t, int32_t, int32_t, tpg_tensor, const uint8_t*, const tpg_tensor*,
+                                      const int32_t*, const int32_t*, const int32_t*, const int32_t*, hipStream_t);
+extern "C" int32_t tpg_maxout_fwd_impl(int32_t, int32_t, tpg_tensor, tpg_tensor, uint8_t*, hipStream_t);
+extern "C" int32_t tpg_maxout_bwd_impl(int32_t, int32_t, tpg_tensor, const uint8_t*, tpg_tensor, hipStream_t);
+extern "C" int32_t tpg_adam_impl(int64_t, float*, const float*, float*, float*, float, float, float, float, float,
+                                  int32_t, float, hipStream_t);
+
+namespace tpg {
+int launch_reflect_fold(int N, int C, int H, int W, int pt, int pb, int pl, int pr, const tpg_tensor& dpad,
+                        const tpg_tensor& dx, hipStream_t s);
+}
+
+using namespace tpg;
+
+static thread_local std::string g_err;
+
+static int32_t fail(int32_t code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+static int32_t hip_check(int e, const char* what) {
+  if (e == 0) return 0;
+  return fail(e > 0 ? e : -100, "%s failed: %s", what, e > 0 ? hipGetErrorString((hipError_t)e) : "bad config");
+}
+
+static inline int esize(int dtype) { return dtype == TPG_BF16 ? 2 : 4; }
+static inline int64_t rup(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline int pmod(int a, int m) { return ((a % m) + m) % m; }
+
+// ------------------------------------------------------------------ problem plans --
+struct Prob {
+  IgemmArgs a;
+  PackArgs pk;
+  int cfg = 0;
+  size_t wp_bytes = 0, sk_bytes = 0;
+};
+
+static int choose_cfg(int nout) {
+  if (nout <= 16) return 0;
+  if (nout <= 32) return 1;
+  if (nout <= 64) return 2;
+  if (nout <= 96) return 3;
+  if (nout <= 128) return 4;
+  if (nout > 192 && nout <= 224) return 5;
+  return 4;
+}
+
+// fill unit / tile / split-K bookkeeping once geometry, C, Nout and taps are known
+static void finish(Prob& P, int dtype, int M) {
+  IgemmArgs& a = P.a;
+  const int upk = dtype == TPG_BF16 ? 4 : 2;
+  a.upt = cdiv(std::max(a.C, 1), 16);
+  a.nunits = a.ntaps > 0 ? (int)rup((int64_t)a.ntaps * a.upt, upk) : 0;
+  a.M = M;
+  P.cfg = choose_cfg(a.Nout);
+  const int bn = igemm_cfg_bn(P.cfg), bm = igemm_cfg_bm(P.cfg);
+  const int npad = (int)rup(a.Nout, bn);
+  P.wp_bytes = (size_t)rup((int64_t)npad * a.nunits * 16 * esize(dtype), 256);
+  const int nkt = a.nunits / upk;
+  const int blocks = cdiv(M, bm) * (npad / bn);
+  a.ksplit = 1;
+  a.kt_per_split = std::max(nkt, 1);
+  if (blocks < 480 && nkt >= 8) {
+    int ks = std::min(cdiv(960, blocks), nkt / 4);
+    if (ks > 1) {
+      a.kt_per_split = cdiv(nkt, ks);
+      a.ksplit = cdiv(nkt, a.kt_per_split);
+    }
+  }
+  P.sk_bytes = a.ksplit > 1 ? (size_t)rup((int64_t)M * a.Nout * 4, 256) : 0;
+  a.div_jw.init(a.JW);
+  a.div_jhjw.init(a.JH * a.JW);
+  PackArgs& k = P.pk;
+  k.Npad = npad;
+  k.Nreal = a.Nout;
+  k.nunits = a.nunits;
+  k.upt = a.upt;
+  k.ntaps = a.ntaps;
+  k.Creal = a.C;
+  k.dtype = dtype;
+}
+
+// direct form: output grid OH x OW (one class), A pixel = o*s + (r - pad)
+static Prob direct_prob(int N, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  Prob P;
+  memset(&P.a, 0, sizeof(P.a));
+  memset(&P.pk, 0, sizeof(P.pk));
+  IgemmArgs& a = P.a;
+  a.JH = OH; a.JW = OW; a.oy0 = 0; a.ox0 = 0; a.osy = 1; a.osx = 1; a.ist_h = sh; a.ist_w = sw;
+  a.ntaps = kh * kw;
+  for (int r = 0; r < kh; ++r)
+    for (int s = 0; s < kw; ++s) {
+      int t = r * kw + s;
+      a.dy[t] = (int8_t)(r - pt); a.dx[t] = (int8_t)(s - pl);
+      P.pk.tr[t] = (int8_t)r; P.pk.ts[t] = (int8_t)s;
+    }
+  (void)N;
+  return P;
+}
+
+// sub-pixel form: out grid OH x OW, class (py, px); A pixel = j + (p + pad - r)/s
+static std::vector<Prob> subpixel_probs(int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  std::vector<Prob> v;
+  for (int py = 0; py < sh; ++py)
+    for (int px = 0; px < sw; ++px) {
+      if (py >= OH || px >= OW) continue;
+      Prob P;
+      memset(&P.a, 0, sizeof(P.a));
+      memset(&P.pk, 0, sizeof(P.pk));
+      IgemmArgs& a = P.a;
+      a.JH = cdiv(OH - py, sh); a.JW = cdiv(OW - px, sw);
+      a.oy0 = py; a.ox0 = px; a.osy = sh; a.osx = sw; a.ist_h = 1; a.ist_w = 1;
+      int t = 0;
+      for (int r = 0; r < kh; ++r) {
+        if (pmod(py + pt - r, sh) != 0) continue;
+        for (int s = 0; s < kw; ++s) {
+          if (pmod(px + pl - s, sw) != 0) continue;
+          a.dy[t] = (int8_t)((py + pt - r) / sh);
+          a.dx[t] = (int8_t)((px + pl - s) / sw);
+          P.pk.tr[t] = (int8_t)r; P.pk.ts[t] = (int8_t)s;
+          ++t;
+        }
+      }
+      a.ntaps = t;
+      v.push_back(P);
+    }
+  return v;
+}
+
+static bool dense_nhwc(const tpg_tensor& t, int C, int H, int W) {
+  return t.stride[1] == 1 && t.stride[3] == C && t.stride[2] == (int64_t)W * C;
+}
+
+static bool vec_ok(const tpg_tensor& t, int dtype) {
+  const int es = esize(dtype);
+  if (t.stride[1] != 1) return false;
+  if (((uintptr_t)t.data) % 16) return false;
+  for (int i : {0, 2, 3})
+    if ((t.stride[i] * es) % 16) return false;
+  return true;
+}
+
+static int32_t check_desc(const tpg_conv_desc* d) {
+  if (!d) return fail(-1, "null descriptor");
+  if (d->n <= 0 || d->in_c <= 0 || d->out_c <= 0 || d->kh <= 0 || d->kw <= 0) return fail(-2, "bad sizes");
+  if (d->stride_h <= 0 || d->stride_w <= 0) return fail(-2, "bad stride");
+  if (d->dtype != TPG_F32 && d->dtype != TPG_BF16) return fail(-3, "bad dtype %d", d->dtype);
+  if (d->kh * d->kw > TPG_MAX_TAPS) return fail(-4, "kernel %dx%d has more than %d taps", d->kh, d->kw, TPG_MAX_TAPS);
+  if (d->transposed) {
+    if (d->pad_mode != TPG_PAD_ZERO) return fail(-5, "reflect padding is only defined for Conv2d");
+    int nh = (d->in_h - 1) * d->stride_h - d->pad_t - d->pad_b + d->kh;
+    int nw = (d->in_w - 1) * d->stride_w - d->pad_l - d->pad_r + d->kw;
+    if (d->out_h < nh || d->out_w < nw || d->out_h >= nh + d->stride_h || d->out_w >= nw + d->stride_w)
+      return fail(-6, "ConvTranspose2d output %dx%d inconsistent with geometry (natural %dx%d)", d->out_h, d->out_w, nh, nw);
+  } else {
+    int oh = (d->in_h + d->pad_t + d->pad_b - d->kh) / d->stride_h + 1;
+    int ow = (d->in_w + d->pad_l + d->pad_r - d->kw) / d->stride_w + 1;
+    if (oh != d->out_h || ow != d->out_w) return fail(-6, "Conv2d output %dx%d != %dx%d", d->out_h, d->out_w, oh, ow);
+    if (d->pad_mode == TPG_PAD_REFLECT &&
+        (d->pad_t >= d->in_h || d->pad_b >= d->in_h || d->pad_l >= d->in_w || d->pad_r >= d->in_w))
+      return fail(-7, "reflection padding must be smaller than the input");
+  }
+  if (std::max(std::abs(d->pad_t), std::abs(d->pad_l)) > 100 || d->kh > 64 || d->kw > 64) return fail(-8, "geometry out of range");
+  return 0;
+}
+
+// ---- forward plans
+static std::vector<Prob> plan_fwd(const tpg_conv_desc* d, bool composite) {
+  std::vector<Prob> v;
+  if (!d->transposed) {
+    if (composite) {
+      Prob P = direct_prob(d->n, 1, 1, 1, 1, 1, 1, 0, 0);
+      P.a.C = d->kh * d->kw * d->in_c;
+      P.a.A_H = 1; P.a.A_W = 1;
+      P.pk.cmode = 2; P.pk.nmode = 0; P.pk.comp_kw = d->kw; P.pk.comp_c = d->in_c;
+      P.a.Nout = d->out_c;
+      finish(P, d->dtype, d->n);
+      v.push_back(P);
+    } else {
+      Prob P = direct_prob(d->n, d->out_h, d->out_w, d->kh, d->kw, d->stride_h, d->stride_w, d->pad_t, d->pad_l);
+      P.a.C = d->in_c; P.a.A_H = d->in_h; P.a.A_W = d->in_w; P.a.Nout = d->out_c;
+      P.a.pad_mode = d->pad_mode;
+      P.pk.nmode = 0; P.pk.cmode = 1;
+      finish(P, d->dtype, d->n * d->out_h * d->out_w);
+      v.push_back(P);
+    }
+  } else {
+    if (composite) {
+      Prob P = direct_prob(d->n, 1, 1, 1, 1, 1, 1, 0, 0);
+      P.a.C = d->in_c; P.a.A_H = 1; P.a.A_W = 1;
+      P.a.Nout = d->kh * d->kw * d->out_c;
+      P.pk.nmode = 2; P.pk.cmode = 0; P.pk.comp_kw = d->kw; P.pk.comp_c = d->out_c;
+      finish(P, d->dtype, d->n);
+      v.push_back(P);
+    } else {
+      for (Prob& P : subpixel_probs(d->out_h, d->out_w, d->kh, d->kw, d->stride_h, d->stride_w, d->pad_t, d->pad_l)) {
+        P.a.C = d->in_c; P.a.A_H = d->in_h; P.a.A_W = d->in_w; P.a.Nout = d->out_c;
+        P.pk.nmode = 1; P.pk.cmode = 0;
+        finish(P, d->dtype, d->n * P.a.JH * P.a.JW);
+        v.push_back(P);
+      }
+    }
+  }
+  return v;
+}
+
+static bool fwd_composite(const tpg_conv_desc* d, const tpg_tensor* x, const tpg_tensor* y) {
+  if (!d->transposed) {
+    if (d->in_h != d->kh || d->in_w != d->kw || d->out_h != 1 || d->out_w != 1) return false;
+    if (d->pad_t || d->pad_b || d->pad_l || d->pad_r || d->pad_mode) return false;
+    if (d->kh == 1 && d->kw == 1) return false;
+    return !x || dense_nhwc(*x, d->in_c, d->in_h, d->in_w);
+  }
+  if (d->in_h != 1 || d->in_w != 1 || d->out_h != d->kh || d->out_w != d->kw) return false;
+  if (d->pad_t || d->pad_b || d->pad_l || d->pad_r) return false;
+  if (d->kh == 1 && d->kw == 1) return false;
+  return !y || dense_nhwc(*y, d->out_c, d->out_h, d->out_w);
+}
+
+// ---- input-gradient plans (geometry of the op's forward; for reflect, the padded input)
+static std::vector<Prob> plan_bwd_data(const tpg_conv_desc* d, bool composite) {
+  std::vector<Prob> v;
+  if (!d->transposed) {
+    if (composite) {  // dX[n][(y,x,ci)] = sum_co g[n][co] W[co][ci][y][x]
+      Prob P = direct_prob(d->n, 1, 1, 1, 1, 1, 1, 0, 0);
+      P.a.C = d->out_c; P.a.A_H = 1; P.a.A_W = 1;
+      P.a.Nout = d->kh * d->kw * d->in_c;
+      P.pk.nmode = 2; P.pk.cmode = 0; P.pk.comp_kw = d->kw; P.pk.comp_c = d->in_c;
+      finish(P, d->dtype, d->n);
+      v.push_back(P);
+    } else {
+      const bool refl = d->pad_mode == TPG_PAD_REFLECT;
+      const int IH = refl ? d->in_h + d->pad_t + d->pad_b : d->in_h;
+      const int IW = refl ? d->in_w + d->pad_l + d->pad_r : d->in_w;
+      const int pt = refl ? 0 : d->pad_t, pl = refl ? 0 : d->pad_l;
+      for (Prob& P : subpixel_probs(IH, IW, d->kh, d->kw, d->stride_h, d->stride_w, pt, pl)) {
+        P.a.C = d->out_c; P.a.A_H = d->out_h; P.a.A_W = d->out_w; P.a.Nout = d->in_c;
+        P.pk.nmode = 1; P.pk.cmode = 0;
+        finish(P, d->dtype, d->n * P.a.JH * P.a.JW);
+        v.push_back(P);
+      }
+    }
+  } else {
+    if (composite) {  // dx[n][ci] = sum_{y,x,co} g[n][(y,x,co)] W[ci][co][y][x]
+      Prob P = direct_prob(d->n, 1, 1, 1, 1, 1, 1, 0, 0);
+      P.a.C = d->kh * d->kw * d->out_c; P.a.A_H = 1; P.a.A_W = 1;
+      P.a.Nout = d->in_c;
+      P.pk.nmode = 0; P.pk.cmode = 2; P.pk.comp_kw = d->kw; P.pk.comp_c = d->out_c;
+      finish(P, d->dtype, d->n);
+      v.push_back(P);
+    } else {
+      Prob P = direct_prob(d->n, d->in_h, d->in_w, d->kh, d->kw, d->stride_h, d->stride_w, d->pad_t, d->pad_l);
+      P.a.C = d->out_c; P.a.A_H = d->out_h; P.a.A_W = d->out_w; P.a.Nout = d->in_c;
+      P.pk.nmode = 0; P.pk.cmode = 1;
+      finish(P, d->dtype, d->n * d->in_h * d->in_w);
+      v.push_back(P);
+    }
+  }
+  return v;
+}
+
+static bool bwd_data_composite(const tpg_conv_desc* d, const tpg_tensor* g, const tpg_tensor* dx) {
+  if (!d->transposed) {
+    if (d->in_h != d->kh || d->in_w != d->kw || d->out_h != 1 || d->out_w != 1) return false;
+    if (d->pad_t || d->pad_b || d->pad_l || d->pad_r || d->pad_mode) return false;
+    if (d->kh == 1 && d->kw == 1) return false;
+    return !dx || dense_nhwc(*dx, d->in_c, d->in_h, d->in_w);
+  }
+  if (d->in_h != 1 || d->in_w != 1 || d->out_h != d->kh || d->out_w != d->kw) return false;
+  if (d->pad_t || d->pad_b || d->pad_l || d->pad_r) return false;
+  if (d->kh == 1 && d->kw == 1) return false;
+  return !g || dense_nhwc(*g, d->out_c, d->out_h, d->out_w);
+}
+
+static size_t probs_ws(const std::vector<Prob>& v) {
+  size_t wp = 0, sk = 0;
+  for (const Prob& P : v) { wp += P.wp_bytes; sk = std::max(sk, P.sk_bytes); }
+  return wp + sk;
+}
+
+static size_t reflect_tmp_bytes(const tpg_conv_desc* d) {
+  if (d->transposed || d->pad_mode != TPG_PAD_REFLECT) return 0;
+  return (size_t)rup((int64_t)d->n * (d->in_h + d->pad_t + d->pad_b) * (d->in_w + d->pad_l + d->pad_r) *
+                         rup(d->in_c, 8) * esize(d->dtype), 256);
+}
+
+extern "C" size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op) {
+  if (check_desc(d)) return 0;
+  if (op == TPG_OP_FWD) {
+    size_t a = probs_ws(plan_fwd(d, false));
+    if (fwd_composite(d, nullptr, nullptr)) a = std::max(a, probs_ws(plan_fwd(d, true)));
+    return a + 256;
+  }
+  if (op == TPG_OP_BWD_DATA) {
+    size_t a = probs_ws(plan_bwd_data(d, false)) + reflect_tmp_bytes(d);
+    if (bwd_data_composite(d, nullptr, nullptr)) a = std::max(a, probs_ws(plan_bwd_data(d, true)));
+    return a + 256;
+  }
+  return 256;  // bwd_filter accumulates straight into dw
+}
+
+// run a list of problems: pack -> [zero split-K] -> igemm -> [finalize]
+static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, const tpg_tensor& W, const float* bias,
+                         int bias_mod, const tpg_tensor& R, float res_scale, const tpg_tensor& Y, int act, float slope,
+                         char* ws, size_t ws_bytes, hipStream_t s) {
+  size_t need = probs_ws(v);
+  if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
+  const bool vA = vec_ok(A, dtype);
+  size_t off = 0;
+  std::vector<char*> wps;
+  for (Prob& P : v) { wps.push_back(ws + off); off += P.wp_bytes; }
+  char* sk = ws + off;
+  for (size_t i = 0; i < v.size(); ++i) {
+    Prob& P = v[i];
+    IgemmArgs& a = P.a;
+    PackArgs& k = P.pk;
+    k.W = reinterpret_cast<const float*>(W.data);
+    k.w_sa = W.stride[0]; k.w_sb = W.stride[1]; k.w_sr = W.stride[2]; k.w_ss = W.stride[3];
+    k.Wp = wps[i];
+    if (a.nunits > 0) {
+      int e = launch_pack(k, s);
+      if (e) return hip_check(e, "pack");
+    }
+    a.A = A.data; a.a_sn = A.stride[0]; a.a_sh = A.stride[2]; a.a_sw = A.stride[3];
+    a.vec_ok = vA;
+    a.Wp = wps[i];
+    a.Y = Y.data; a.y_sn = Y.stride[0]; a.y_sh = Y.stride[2]; a.y_sw = Y.stride[3];
+    a.bias = bias; a.bias_mod = bias_mod;
+    a.R = R.data; a.r_sn = R.stride[0]; a.r_sh = R.stride[2]; a.r_sw = R.stride[3];
+    a.res_scale = res_scale; a.act = act; a.slope = slope;
+    a.ws = nullptr;
+    if (a.ksplit > 1) {
+      a.ws = reinterpret_cast<float*>(sk);
+      hipError_t e = hipMemsetAsync(sk, 0, (size_t)a.M * a.Nout * 4, s);
+      if (e) return hip_check((int)e, "hipMemsetAsync");
+    }
+    int e = launch_igemm(a, dtype, P.cfg, s);
+    if (e) return hip_check(e, "igemm");
+    if (a.ksplit > 1) {
+      EpiArgs ep;
+      ep.ws = a.ws; ep.M = a.M; ep.Nout = a.Nout; ep.JH = a.JH; ep.JW = a.JW;
+      ep.Y = a.Y; ep.y_sn = a.y_sn; ep.y_sh = a.y_sh; ep.y_sw = a.y_sw;
+      ep.oy0 = a.oy0; ep.ox0 = a.ox0; ep.osy = a.osy; ep.osx = a.osx;
+      ep.bias = bias; ep.bias_mod = bias_mod;
+      ep.R = a.R; ep.r_sn = a.r_sn; ep.r_sh = a.r_sh; ep.r_sw = a.r_sw;
+      ep.res_scale = res_scale; ep.act = act; ep.slope = slope; ep.dtype = dtype;
+      e = launch_epilogue(ep, s);
+      if (e) return hip_check(e, "epilogue");
+    }
+  }
+  return 0;
+}
+
+static int32_t check_tensor(const tpg_tensor& t, int dtype, const char* name) {
+  if (!t.data) return fail(-10, "%s is NULL", name);
+  if (t.dtype != dtype) return fail(-11, "%s dtype %d != %d", name, t.dtype, dtype);
+  if (t.stride[1] != 1) return fail(-12, "%s must be channels-last (channel stride 1), got %lld", name,
+                                    (long long)t.stride[1]);
+  return 0;
+}
+
+extern "C" int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, const float* bias,
+                                  tpg_tensor residual, tpg_tensor y, void* ws, size_t ws_bytes, tpg_stream_t stream) {
+  int32_t rc = check_desc(d);
+  if (rc) return rc;
+  if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(y, d->dtype, "y"))) return rc;
+  if (!w.data || w.dtype != TPG_F32) return fail(-13, "weight must be fp32");
+  if (residual.data && (rc = check_tensor(residual, d->dtype, "residual"))) return rc;
+  const bool comp = fwd_composite(d, &x, &y);
+  std::vector<Prob> v = plan_fwd(d, comp);
+  int bias_mod = (comp && d->transposed) ? d->out_c : 0;
+  if (comp && residual.data) return fail(-14, "residual not supported on a full-kernel conv");
+  return run_probs(v, d->dtype, x, w, bias, bias_mod, residual, d->res_scale, y, d->act, d->slope,
+                   reinterpret_cast<char*>(ws), ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx, void* ws,
+                                       size_t ws_bytes, tpg_stream_t stream) {
+  int32_t rc = check_desc(d);
+  if (rc) return rc;
+  if ((rc = check_tensor(g, d->dtype, "g")) || (rc = check_tensor(dx, d->dtype, "dx"))) return rc;
+  if (!w.data || w.dtype != TPG_F32) return fail(-13, "weight must be fp32");
+  hipStream_t s = (hipStream_t)stream;
+  const bool comp = bwd_data_composite(d, &g, &dx);
+  std::vector<Prob> v = plan_bwd_data(d, comp);
+  tpg_tensor none;
+  memset(&none, 0, sizeof(none));
+  const bool refl = !comp && !d->transposed && d->pad_mode == TPG_PAD_REFLECT;
+  if (!refl)
+    return run_probs(v, d->dtype, g, w, nullptr, 0, none, 0.f, dx, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws),
+                     ws_bytes, s);
+  // reflect: gradient of the padded input into a dense NHWC temp, then fold onto dx
+  const size_t tmpb = reflect_tmp_bytes(d);
+  if (ws_bytes < tmpb) return fail(-20, "workspace too small");
+  const int PH = d->in_h + d->pad_t + d->pad_b, PW = d->in_w + d->pad_l + d->pad_r, Cp = (int)rup(d->in_c, 8);
+  tpg_tensor tmp;
+  memset(&tmp, 0, sizeof(tmp));
+  tmp.data = ws; tmp.dtype = d->dtype;
+  tmp.stride[0] = (int64_t)PH * PW * Cp; tmp.stride[1] = 1; tmp.stride[2] = (int64_t)PW * Cp; tmp.stride[3] = Cp;
+  rc = run_probs(v, d->dtype, g, w, nullptr, 0, none, 0.f, tmp, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws) + tmpb,
+                 ws_bytes - tmpb, s);
+  if (rc) return rc;
+  return hip_check(launch_reflect_fold(d->n, d->in_c, d->in_h, d->in_w, d->pad_t, d->pad_b, d->pad_l, d->pad_r, tmp, dx, s),
+                   "reflect_fold");
+}
+
+extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw, void* ws,
+                                         size_t ws_bytes, tpg_stream_t stream) {
+  (void)ws; (void)ws_bytes;
+  int32_t rc = check_desc(d);
+  if (rc) return rc;
+  if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(g, d->dtype, "g"))) return rc;
+  if (!dw.data || dw.dtype != TPG_F32) return fail(-13, "dw must be fp32");
+  WgradArgs a;
+  memset(&a, 0, sizeof(a));
+  const tpg_tensor& P = d->transposed ? x : g;  // iteration grid operand
+  const tpg_tensor& Q = d->transposed ? g : x;  // gathered operand
+  const int PH = d->transposed ? d->in_h : d->out_h, PW = d->transposed ? d->in_w : d->out_w;
+  const int QH = d->transposed ? d->out_h : d->in_h, QW = d->transposed ? d->out_w : d->in_w;
+  const int Ca = d->transposed ? d->in_c : d->out_c, cb = d->transposed ? d->out_c : d->in_c;
+  const bool comp = d->transposed ? bwd_data_composite(d, &g, nullptr) : fwd_composite(d, &x, nullptr);
+  a.P = P.data; a.p_sn = P.stride[0]; a.p_sh = P.stride[2]; a.p_sw = P.stride[3];
+  a.Q = Q.data; a.q_sn = Q.stride[0]; a.q_sh = Q.stride[2]; a.q_sw = Q.stride[3];
+  a.Ca = Ca;
+  a.vec_p = vec_ok(P, d->dtype);
+  a.vec_q = vec_ok(Q, d->dtype);
+  if (comp) {
+    a.PH = 1; a.PW = 1; a.QH = 1; a.QW = 1;
+    a.Cb = d->kh * d->kw * cb;
+    a.bcomp = 1; a.comp_kw = d->kw; a.comp_cb = cb;
+    a.ntaps = 1; a.dy[0] = 0; a.dx[0] = 0; a.tr[0] = 0; a.ts[0] = 0;
+    a.qst_h = 1; a.qst_w = 1;
+  } else {
+    a.PH = PH; a.PW = PW; a.QH = QH; a.QW = QW; a.Cb = cb;
+    a.qst_h = d->stride_h; a.qst_w = d->stride_w;
+    a.pad_mode = d->transposed ? 0 : d->pad_mode;
+    a.ntaps = d->kh * d->kw;
+    for (int r = 0; r < d->kh; ++r)
+      for (int s = 0; s < d->kw; ++s) {
+        int t = r * d->kw + s;
+        a.dy[t] = (int8_t)(r - d->pad_t); a.dx[t] = (int8_t)(s - d->pad_l);
+        a.tr[t] = (int8_t)r; a.ts[t] = (int8_t)s;
+      }
+  }
+  a.npix = d->n * a.PH * a.PW;
+  a.dW = reinterpret_cast<float*>(dw.data);
+  a.w_sa = dw.stride[0]; a.w_sb = dw.stride[1]; a.w_sr = dw.stride[2]; a.w_ss = dw.stride[3];
+  a.div_pw.init(a.PW);
+  a.div_phpw.init(a.PH * a.PW);
+  const int cfg = (a.Ca >= 128 && a.Cb >= 128) ? 1 : 0;
+  const int bm = wgrad_cfg_bm(cfg), bn = wgrad_cfg_bn(cfg);
+  const int tiles = cdiv(a.Ca, bm) * cdiv(a.Cb, bn) * a.ntaps;
+  int ks = std::max(1, cdiv(1536, tiles));
+  ks = std::min(ks, std::max(1, a.npix / (32 * 16)));
+  a.pix_per_split = (int)rup(cdiv(a.npix, ks), 32);
+  a.ksplit = cdiv(a.npix, a.pix_per_split);
+  return hip_check(launch_wgrad(a, d->dtype, cfg, (hipStream_t)stream), "wgrad");
+}
+
+extern "C" int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope, tpg_tensor gy,
+                               tpg_tensor y, tpg_tensor g, float* dbias, tpg_stream_t stream) {
+  if (!gy.data || !g.data || (act != TPG_ACT_NONE && !y.data)) return fail(-10, "act_bwd: NULL tensor");
+  return hip_check(tpg_act_bwd_impl(n, c, h, w, act, slope, gy, y, g, dbias, (hipStream_t)stream), "act_bwd");
+}
+
+extern "C" int32_t tpg_copy4d(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor in, tpg_tensor out,
+                              tpg_stream_t stream) {
+  if (!in.data || !out.data) return fail(-10, "copy4d: NULL tensor");
+  if ((int64_t)n * c * h * w == 0) return 0;
+  return hip_check(tpg_copy4d_impl(n, c, h, w, in, out, (hipStream_t)stream), "copy4d");
+}
+
+extern "C" int32_t tpg_local_fuse_fwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, const tpg_tensor* parts,
+                                      const int32_t* ph, const int32_t* pw, const int32_t* top, const int32_t* left,
+                                      tpg_tensor y, uint8_t* argmax, tpg_stream_t stream) {
+  for (int k = 0; k < 4; ++k)
+    if (!parts[k].data) return fail(-10, "local_fuse: part %d NULL", k);
+  return hip_check(tpg_fuse_fwd_impl(n, c, out_h, out_w, parts, ph, pw, top, left, y, argmax, (hipStream_t)stream),
+                   "local_fuse_fwd");
+}
+
+extern "C" int32_t tpg_local_fuse_bwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, tpg_tensor gy,
+                                      const uint8_t* argmax, const tpg_tensor* dparts, const int32_t* ph,
+                                      const int32_t* pw, const int32_t* top, const int32_t* left, tpg_stream_t stream) {
+  if (!argmax || !gy.data) return fail(-10, "local_fuse_bwd: NULL");
+  return hip_check(tpg_fuse_bwd_impl(n, c, out_h, out_w, gy, argmax, dparts, ph, pw, top, left, (hipStream_t)stream),
+                   "local_fuse_bwd");
+}
+
+extern "C" int32_t tpg_maxout2_fwd(int32_t b, int32_t m, tpg_tensor x, tpg_tensor y, uint8_t* argmax,
+                                   tpg_stream_t stream) {
+  return hip_check(tpg_maxout_fwd_impl(b, m, x, y, argmax, (hipStream_t)stream), "maxout_fwd");
+}
+
+extern "C" int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argmax, tpg_tensor dx,
+                                   tpg_stream_t stream) {
+  return hip_check(tpg_maxout_bwd_impl(b, m, gy, argmax, dx, (hipStream_t)stream), "maxout_bwd");
+}
+
+extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                            float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
+                            float grad_scale, tpg_stream_t stream) {
+  if (numel == 0) return 0;
+  return hip_check(tpg_adam_impl(numel, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step,
+                                 grad_scale, (hipStream_t)stream),
+                   "adam");
+}
+
+extern "C" const char* tpg_version(void) { return "tpgan_hip 0.1 gfx950"; }
+extern "C" const char* tpg_last_error(void) { return g_err.c_str(); }

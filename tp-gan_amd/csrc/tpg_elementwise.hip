@@ -1,0 +1,320 @@
+// HBM-bound kernels of the TP-GAN hot path (gfx950): weight packing, activation
+// backward + bias gradient, strided copy / concat / dtype conversion, LocalFuser,
+// maxout, reflection-pad fold and the Adam update.  Each is a grid-stride loop over
+// channels-last elements so that consecutive lanes touch consecutive channels.
+#include "tpg_internal.h"
+#include "../../include/tpgan.h"
+
+namespace tpg {
+
+__device__ __forceinline__ float ld_any(const void* p, int dtype, int64_t off) {
+  return dtype == TPG_BF16 ? (float)reinterpret_cast<const __bf16*>(p)[off] : reinterpret_cast<const float*>(p)[off];
+}
+__device__ __forceinline__ void st_any(void* p, int dtype, int64_t off, float v) {
+  if (dtype == TPG_BF16) reinterpret_cast<__bf16*>(p)[off] = (__bf16)v;
+  else reinterpret_cast<float*>(p)[off] = v;
+}
+
+static inline int grid_for(int64_t total, int per_block = 256, int cap = 8192) {
+  int64_t b = (total + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
+// ------------------------------------------------------------------ weight packing --
+__global__ __launch_bounds__(256) void pack_kernel(const PackArgs p) {
+  const int64_t row_len = (int64_t)p.nunits * 16;
+  const int64_t total = (int64_t)p.Npad * row_len;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int np = (int)(idx / row_len);
+    const int kk = (int)(idx - (int64_t)np * row_len);
+    const int unit = kk >> 4;
+    const int tap = unit / p.upt;
+    const int cp = (unit - tap * p.upt) * 16 + (kk & 15);
+    float v = 0.f;
+    if (np < p.Nreal && tap < p.ntaps && cp < p.Creal) {
+      int a = 0, b = 0, r = p.tr[tap < TPG_MAX_TAPS ? tap : 0], s = p.ts[tap < TPG_MAX_TAPS ? tap : 0];
+      // decode n'
+      if (p.nmode == 0) a = np;
+      else if (p.nmode == 1) b = np;
+      else {
+        int rs = np / p.comp_c, ch = np - rs * p.comp_c;
+        r = rs / p.comp_kw; s = rs - r * p.comp_kw;
+        if (p.nmode == 2) b = ch; else a = ch;
+      }
+      // decode c'
+      if (p.cmode == 0) a = cp;
+      else if (p.cmode == 1) b = cp;
+      else {
+        int rs = cp / p.comp_c, ch = cp - rs * p.comp_c;
+        r = rs / p.comp_kw; s = rs - r * p.comp_kw;
+        if (p.cmode == 2) b = ch; else a = ch;
+      }
+      v = p.W[a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss];
+    }
+    st_any(p.Wp, p.dtype, idx, v);
+  }
+}
+
+int launch_pack(const PackArgs& a, hipStream_t s) {
+  int64_t total = (int64_t)a.Npad * a.nunits * 16;
+  hipLaunchKernelGGL(pack_kernel, dim3(grid_for(total)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------------------- activation backward + bias grad --
+// g = gy * act'(y); 64 channels x 4 pixel lanes per block, dbias reduced in LDS and
+// added with one atomic per channel per block.
+__global__ __launch_bounds__(256) void act_bwd_kernel(int N, int C, int H, int W, int act, float slope,
+                                                      tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int64_t npix = (int64_t)N * H * W;
+  float sum = 0.f;
+  if (c < C) {
+    for (int64_t pix = blockIdx.x * 4 + pl; pix < npix; pix += (int64_t)gridDim.x * 4) {
+      int n = (int)(pix / ((int64_t)H * W));
+      int rem = (int)(pix - (int64_t)n * H * W);
+      int h = rem / W, w = rem - (rem / W) * W;
+      float v = ld_any(gy.data, gy.dtype, n * gy.stride[0] + c * gy.stride[1] + h * gy.stride[2] + w * gy.stride[3]);
+      if (act != TPG_ACT_NONE) {
+        float yv = ld_any(y.data, y.dtype, n * y.stride[0] + c * y.stride[1] + h * y.stride[2] + w * y.stride[3]);
+        if (!(yv > 0.f)) v = (act == TPG_ACT_LEAKY) ? v * slope : 0.f;
+      }
+      st_any(g.data, g.dtype, n * g.stride[0] + c * g.stride[1] + h * g.stride[2] + w * g.stride[3], v);
+      sum += v;
+    }
+  }
+  red[pl][cl] = sum;
+  __syncthreads();
+  if (pl == 0 && c < C && dbias) {
+    float s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    atomicAdd(dbias + c, s);
+  }
+}
+
+// ------------------------------------------------------------ strided 4-D copy --
+__global__ __launch_bounds__(256) void copy4d_kernel(int N, int C, int H, int W, tpg_tensor in, tpg_tensor out) {
+  const int64_t total = (int64_t)N * C * H * W;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    // channel fastest (channels-last order)
+    int c = (int)(idx % C);
+    int64_t pix = idx / C;
+    int w = (int)(pix % W);
+    int64_t t = pix / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float v = ld_any(in.data, in.dtype, n * in.stride[0] + c * in.stride[1] + h * in.stride[2] + w * in.stride[3]);
+    st_any(out.data, out.dtype, n * out.stride[0] + c * out.stride[1] + h * out.stride[2] + w * out.stride[3], v);
+  }
+}
+
+// ------------------------------------------------------------------ LocalFuser --
+struct FuseGeom {
+  tpg_tensor part[4];
+  int ph[4], pw[4], top[4], left[4];
+};
+
+__global__ __launch_bounds__(256) void fuse_fwd_kernel(int N, int C, int OH, int OW, FuseGeom g, tpg_tensor y,
+                                                       uint8_t* amax) {
+  const int64_t total = (int64_t)N * OH * OW * C;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(idx % C);
+    int64_t pix = idx / C;
+    int x = (int)(pix % OW);
+    int64_t t = pix / OW;
+    int yy = (int)(t % OH);
+    int n = (int)(t / OH);
+    float best = 0.f;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int py = yy - g.top[k], px = x - g.left[k];
+      float v = 0.f;
+      if ((unsigned)py < (unsigned)g.ph[k] && (unsigned)px < (unsigned)g.pw[k]) {
+        const tpg_tensor& P = g.part[k];
+        v = ld_any(P.data, P.dtype, n * P.stride[0] + c * P.stride[1] + py * P.stride[2] + px * P.stride[3]);
+      }
+      if (k == 0 || v > best || (v != v && best == best)) { best = v; arg = k; }
+    }
+    st_any(y.data, y.dtype, n * y.stride[0] + c * y.stride[1] + yy * y.stride[2] + x * y.stride[3], best);
+    if (amax) amax[idx] = (uint8_t)arg;
+  }
+}
+
+__global__ __launch_bounds__(256) void fuse_bwd_kernel(int N, int C, int OH, int OW, int k, tpg_tensor gy,
+                                                       const uint8_t* amax, tpg_tensor dpart, int ph, int pw, int top,
+                                                       int left) {
+  const int64_t total = (int64_t)N * ph * pw * C;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(idx % C);
+    int64_t pix = idx / C;
+    int px = (int)(pix % pw);
+    int64_t t = pix / pw;
+    int py = (int)(t % ph);
+    int n = (int)(t / ph);
+    int yy = py + top, x = px + left;
+    float v = 0.f;
+    if ((unsigned)yy < (unsigned)OH && (unsigned)x < (unsigned)OW) {
+      int64_t cidx = (((int64_t)n * OH + yy) * OW + x) * C + c;
+      if (amax[cidx] == k)
+        v = ld_any(gy.data, gy.dtype, n * gy.stride[0] + c * gy.stride[1] + yy * gy.stride[2] + x * gy.stride[3]);
+    }
+    st_any(dpart.data, dpart.dtype,
+           n * dpart.stride[0] + c * dpart.stride[1] + py * dpart.stride[2] + px * dpart.stride[3], v);
+  }
+}
+
+// ---------------------------------------------------------------------- maxout --
+__global__ __launch_bounds__(256) void maxout_fwd_kernel(int B, int M, tpg_tensor x, tpg_tensor y, uint8_t* amax) {
+  const int64_t total = (int64_t)B * M;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int b = (int)(idx / M), j = (int)(idx % M);
+    float v0 = ld_any(x.data, x.dtype, b * x.stride[0] + (2 * j) * x.stride[1]);
+    float v1 = ld_any(x.data, x.dtype, b * x.stride[0] + (2 * j + 1) * x.stride[1]);
+    bool second = (v1 > v0) || (v1 != v1 && v0 == v0);
+    st_any(y.data, y.dtype, b * y.stride[0] + j * y.stride[1], second ? v1 : v0);
+    if (amax) amax[idx] = second ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxout_bwd_kernel(int B, int M, tpg_tensor gy, const uint8_t* amax,
+                                                         tpg_tensor dx) {
+  const int64_t total = (int64_t)B * 2 * M;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int b = (int)(idx / (2 * M)), i = (int)(idx % (2 * M));
+    int j = i >> 1;
+    float v = 0.f;
+    if (amax[(int64_t)b * M + j] == (i & 1)) v = ld_any(gy.data, gy.dtype, b * gy.stride[0] + j * gy.stride[1]);
+    st_any(dx.data, dx.dtype, b * dx.stride[0] + i * dx.stride[1], v);
+  }
+}
+
+// -------------------------------------------------- reflection-pad gradient fold --
+// dx[n, iy, ix, c] = sum of dpad at every padded position that reads (iy, ix).
+__global__ __launch_bounds__(256) void reflect_fold_kernel(int N, int C, int H, int W, int pt, int pb, int pl, int pr,
+                                                           tpg_tensor dpad, tpg_tensor dx) {
+  const int64_t total = (int64_t)N * H * W * C;
+  const int PH = H + pt + pb, PW = W + pl + pr;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(idx % C);
+    int64_t pix = idx / C;
+    int ix = (int)(pix % W);
+    int64_t t = pix / W;
+    int iy = (int)(t % H);
+    int n = (int)(t / H);
+    int ys[3], xs[3], ny = 0, nx = 0;
+    ys[ny++] = iy + pt;
+    if (iy >= 1 && iy <= pt) ys[ny++] = pt - iy;
+    if (iy <= H - 2 && iy >= H - 1 - pb) { int q = 2 * H - 2 - iy + pt; if (q < PH) ys[ny++] = q; }
+    xs[nx++] = ix + pl;
+    if (ix >= 1 && ix <= pl) xs[nx++] = pl - ix;
+    if (ix <= W - 2 && ix >= W - 1 - pr) { int q = 2 * W - 2 - ix + pl; if (q < PW) xs[nx++] = q; }
+    float v = 0.f;
+    for (int a = 0; a < ny; ++a)
+      for (int b = 0; b < nx; ++b)
+        v += ld_any(dpad.data, dpad.dtype,
+                    n * dpad.stride[0] + c * dpad.stride[1] + ys[a] * dpad.stride[2] + xs[b] * dpad.stride[3]);
+    st_any(dx.data, dx.dtype, n * dx.stride[0] + c * dx.stride[1] + iy * dx.stride[2] + ix * dx.stride[3], v);
+  }
+}
+
+int launch_reflect_fold(int N, int C, int H, int W, int pt, int pb, int pl, int pr, const tpg_tensor& dpad,
+                        const tpg_tensor& dx, hipStream_t s) {
+  hipLaunchKernelGGL(reflect_fold_kernel, dim3(grid_for((int64_t)N * H * W * C)), dim3(256), 0, s, N, C, H, W, pt,
+                     pb, pl, pr, dpad, dx);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------- Adam --
+// torch.optim.Adam (amsgrad=False, maximize=False): g += wd * p; m = b1 m + (1-b1) g;
+// v = b2 v + (1-b2) g^2; p -= lr / (1-b1^t) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
+__global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ gr,
+                                                   float* __restrict__ m, float* __restrict__ v, float lr, float b1,
+                                                   float b2, float eps, float wd, float bc1, float bc2s, float gscale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float g = gr[i] * gscale;
+    float pv = p[i];
+    if (wd != 0.f) g += wd * pv;
+    float mv = b1 * m[i] + (1.f - b1) * g;
+    float vv = b2 * v[i] + (1.f - b2) * g * g;
+    m[i] = mv;
+    v[i] = vv;
+    float denom = sqrtf(vv) / bc2s + eps;
+    p[i] = pv - (lr / bc1) * mv / denom;
+  }
+}
+
+}  // namespace tpg
+
+using namespace tpg;
+
+extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
+                                     tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, hipStream_t s) {
+  int64_t npix = (int64_t)n * h * w;
+  int gx = (int)std::min<int64_t>((npix + 63) / 64, 2048);
+  if (gx < 1) gx = 1;
+  dim3 grid(gx, (c + 63) / 64);
+  hipLaunchKernelGGL(act_bwd_kernel, grid, dim3(256), 0, s, n, c, h, w, act, slope, gy, y, g, dbias);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_copy4d_impl(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor in, tpg_tensor out,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(copy4d_kernel, dim3(grid_for((int64_t)n * c * h * w)), dim3(256), 0, s, n, c, h, w, in, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_fuse_fwd_impl(int32_t n, int32_t c, int32_t oh, int32_t ow, const tpg_tensor* parts,
+                                      const int32_t* ph, const int32_t* pw, const int32_t* top, const int32_t* left,
+                                      tpg_tensor y, uint8_t* amax, hipStream_t s) {
+  FuseGeom g;
+  for (int k = 0; k < 4; ++k) {
+    g.part[k] = parts[k]; g.ph[k] = ph[k]; g.pw[k] = pw[k]; g.top[k] = top[k]; g.left[k] = left[k];
+  }
+  hipLaunchKernelGGL(fuse_fwd_kernel, dim3(grid_for((int64_t)n * oh * ow * c)), dim3(256), 0, s, n, c, oh, ow, g, y,
+                     amax);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_fuse_bwd_impl(int32_t n, int32_t c, int32_t oh, int32_t ow, tpg_tensor gy, const uint8_t* amax,
+                                      const tpg_tensor* dparts, const int32_t* ph, const int32_t* pw,
+                                      const int32_t* top, const int32_t* left, hipStream_t s) {
+  for (int k = 0; k < 4; ++k) {
+    if (!dparts[k].data) continue;
+    hipLaunchKernelGGL(fuse_bwd_kernel, dim3(grid_for((int64_t)n * ph[k] * pw[k] * c)), dim3(256), 0, s, n, c, oh,
+                       ow, k, gy, amax, dparts[k], ph[k], pw[k], top[k], left[k]);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_maxout_fwd_impl(int32_t b, int32_t m, tpg_tensor x, tpg_tensor y, uint8_t* amax, hipStream_t s) {
+  hipLaunchKernelGGL(maxout_fwd_kernel, dim3(grid_for((int64_t)b * m)), dim3(256), 0, s, b, m, x, y, amax);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_maxout_bwd_impl(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* amax, tpg_tensor dx,
+                                        hipStream_t s) {
+  hipLaunchKernelGGL(maxout_bwd_kernel, dim3(grid_for((int64_t)b * 2 * m)), dim3(256), 0, s, b, m, gy, amax, dx);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_adam_impl(int64_t numel, float* param, const float* grad, float* m, float* v, float lr,
+                                  float b1, float b2, float eps, float wd, int32_t step, float gscale, hipStream_t s) {
+  float bc1 = 1.f - powf(b1, (float)step);
+  float bc2s = sqrtf(1.f - powf(b2, (float)step));
+  int blocks = (int)std::min<int64_t>((numel + 255) / 256, 8192);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, bc1,
+                     bc2s, gscale);
+  return (int)hipGetLastError();
+}

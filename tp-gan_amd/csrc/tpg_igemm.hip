@@ -1,0 +1,324 @@
+// Tap-table implicit-GEMM convolution for gfx950 (CDNA4), NHWC activations.
+//
+// One kernel family covers every conv-shaped op of the TP-GAN hot path
+// (SURVEY.md §2 op-class table):
+//   Conv2d forward                 rows = output pixels, taps = (r - pad) offsets, input stride s
+//   Conv2d input gradient          rows = one parity class of input pixels, taps = the kernel
+//                                  positions that reach that class (sub-pixel decomposition)
+//   ConvTranspose2d forward        same as the Conv2d input gradient
+//   ConvTranspose2d input gradient same as the Conv2d forward
+//   Linear / full-kernel conv      one tap, channels = flattened (y, x, c)
+//
+// GEMM view: Out[row][n'] = sum_{tap, c} A[pix(row, tap)][c] * Wp[n'][tap][c].
+// K is walked in 16-channel units of one tap; one k-tile = 128 bytes per row
+// (bf16: 4 units = 64 k, f32: 2 units = 32 k).  A rows are gathered from HBM into
+// registers (zero outside the image, or reflected), staged through a double-buffered,
+// XOR-swizzled LDS image; weights are pre-packed [n'][unit][16] so their tile rows are
+// contiguous 128-byte lines.
+//
+// MFMA: bf16 -> v_mfma_f32_16x16x32_bf16; f32 (parity mode) -> v_mfma_f32_16x16x4_f32
+// (exact f32 FMA chain).  Both read one 16-byte LDS chunk per lane per operand: lane l
+// holds row (l & 15), chunk (4s + (l >> 4)); the f32 form issues 4 MFMAs over the chunk's
+// 4 elements, so A and B agree on the k permutation and the sum is over all of K.
+//
+// Epilogue (fused): + bias, + res_scale * residual, LeakyReLU / ReLU, dtype convert,
+// store into any (n, h, w) strided NHWC view (a channel slice implements zero-copy
+// output into a concat buffer).  Split-K blocks atomically add fp32 partials into a work
+// space instead; tpg_epilogue_kernel finishes them.
+#include "tpg_internal.h"
+#include <type_traits>
+
+namespace tpg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+  if (act == 2) return v > 0.f ? v : v * slope;
+  if (act == 1) return v > 0.f ? v : 0.f;
+  return v;
+}
+
+template <typename E>
+__device__ __forceinline__ float ld_f(const E* p) { return (float)(*p); }
+
+template <typename E>
+__device__ __forceinline__ void st_f(E* p, float v) { *p = (E)v; }
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+template <bool BF, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
+  using E = typename std::conditional<BF, __bf16, float>::type;
+  constexpr int EPC = 16 / sizeof(E);      // elements per 16-byte chunk
+  constexpr int CPU = 16 / EPC;            // chunks per 16-channel unit
+  constexpr int UPK = 8 / CPU;             // units per 128-byte k-tile
+  constexpr int RA = BM / 32;              // A rows staged per thread
+  constexpr int RB = (BN + 31) / 32;       // B rows staged per thread
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MREP = WTM / 16, NREP = WTN / 16;
+  static_assert(MREP * 16 * WM == BM && NREP * 16 * WN == BN, "tile");
+  static_assert(WM * WN == 4, "4 waves");
+
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * (BM + BN) * 8];
+  __shared__ int8_t s_dy[TPG_MAX_TAPS], s_dx[TPG_MAX_TAPS];
+
+  const int tid = threadIdx.x;
+  if (tid < TPG_MAX_TAPS) { s_dy[tid] = p.dy[tid]; s_dx[tid] = p.dx[tid]; }
+
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nkt = p.nunits / UPK;
+  int kt0 = blockIdx.z * p.kt_per_split;
+  int kt1 = min(nkt, kt0 + p.kt_per_split);
+
+  // ---- per-thread staging geometry
+  const int chunk = tid & 7;
+  const int rsub = tid >> 3;
+  const int slot = chunk / CPU;
+  const int part = chunk % CPU;
+  const E* Ag = reinterpret_cast<const E*>(p.A);
+  int64_t a_base[RA];
+  int by[RA], bx[RA];
+  bool rv[RA];
+  const int JHJW = p.JH * p.JW;
+#pragma unroll
+  for (int q = 0; q < RA; ++q) {
+    int row = m0 + rsub + 32 * q;
+    rv[q] = row < p.M;
+    int rr = rv[q] ? row : 0;
+    int n = p.div_jhjw.div(rr);
+    int rem = rr - n * JHJW;
+    int j = p.div_jw.div(rem);
+    int i = rem - j * p.JW;
+    a_base[q] = (int64_t)n * p.a_sn;
+    by[q] = j * p.ist_h;
+    bx[q] = i * p.ist_w;
+  }
+  const E* Wg = reinterpret_cast<const E*>(p.Wp);
+  const int64_t wrow = (int64_t)p.nunits * 16;
+
+  uint4 ra[RA], rb[RB];
+  int tap = 0, cu = 0;
+  {
+    int u = kt0 * UPK + slot;
+    tap = u / p.upt;
+    cu = u - tap * p.upt;
+  }
+
+  auto load_tile = [&](int kt) {
+    // A gather
+    const int c = cu * 16 + part * EPC;
+    const bool tap_ok = tap < p.ntaps;
+    const int dy = tap_ok ? s_dy[tap] : 0;
+    const int dx = tap_ok ? s_dx[tap] : 0;
+#pragma unroll
+    for (int q = 0; q < RA; ++q) {
+      int iy = by[q] + dy, ix = bx[q] + dx;
+      if (p.pad_mode) { iy = reflect_idx(iy, p.A_H); ix = reflect_idx(ix, p.A_W); }
+      bool ok = tap_ok && rv[q] && (unsigned)iy < (unsigned)p.A_H && (unsigned)ix < (unsigned)p.A_W && c < p.C;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ok) {
+        const E* src = Ag + a_base[q] + (int64_t)iy * p.a_sh + (int64_t)ix * p.a_sw + c;
+        if (p.vec_ok && c + EPC <= p.C) {
+          v = *reinterpret_cast<const uint4*>(src);
+        } else {
+          union { uint4 u; E e[EPC]; } t;
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) t.e[e] = (c + e < p.C) ? src[e] : (E)0.f;
+          v = t.u;
+        }
+      }
+      ra[q] = v;
+    }
+    // B (packed weights, always in range)
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      int nr = rsub + 32 * q;
+      if (nr < BN) {
+        const E* src = Wg + (int64_t)(n0 + nr) * wrow + (int64_t)kt * (UPK * 16) + chunk * EPC;
+        rb[q] = *reinterpret_cast<const uint4*>(src);
+      }
+    }
+    // advance unit cursor by one k-tile
+    cu += UPK;
+    while (cu >= p.upt) { cu -= p.upt; ++tap; }
+  };
+
+  auto store_tile = [&](int buf) {
+    uint4* As = lds + buf * (BM + BN) * 8;
+    uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int q = 0; q < RA; ++q) {
+      int r = rsub + 32 * q;
+      As[r * 8 + (chunk ^ ((r >> 1) & 7))] = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      int r = rsub + 32 * q;
+      if (r < BN) Bs[r * 8 + (chunk ^ ((r >> 1) & 7))] = rb[q];
+    }
+  };
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  f32x4 acc[MREP][NREP];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m)
+#pragma unroll
+    for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint4* As = lds + buf * (BM + BN) * 8;
+    const uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 af[MREP], bfr[NREP];
+      const int ch = 4 * s + g;
+#pragma unroll
+      for (int m = 0; m < MREP; ++m) {
+        int r = wm * WTM + m * 16 + r16;
+        af[m] = As[r * 8 + (ch ^ ((r >> 1) & 7))];
+      }
+#pragma unroll
+      for (int n = 0; n < NREP; ++n) {
+        int r = wn * WTN + n * 16 + r16;
+        bfr[n] = Bs[r * 8 + (ch ^ ((r >> 1) & 7))];
+      }
+#pragma unroll
+      for (int m = 0; m < MREP; ++m)
+#pragma unroll
+        for (int n = 0; n < NREP; ++n) {
+          if constexpr (BF) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[m]),
+                                                                __builtin_bit_cast(bf16x8, bfr[n]), acc[m][n], 0, 0, 0);
+          } else {
+            f32x4 a4 = __builtin_bit_cast(f32x4, af[m]);
+            f32x4 b4 = __builtin_bit_cast(f32x4, bfr[n]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], acc[m][n], 0, 0, 0);
+          }
+        }
+    }
+  };
+
+  __syncthreads();  // tap table visible
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      compute(cur);
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue
+  E* Y = reinterpret_cast<E*>(p.Y);
+  const E* R = reinterpret_cast<const E*>(p.R);
+#pragma unroll
+  for (int m = 0; m < MREP; ++m) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int row = m0 + wm * WTM + m * 16 + 4 * g + reg;
+      if (row >= p.M) continue;
+      int n = p.div_jhjw.div(row);
+      int rem = row - n * JHJW;
+      int j = p.div_jw.div(rem);
+      int i = rem - j * p.JW;
+      int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
+      int64_t yoff = (int64_t)n * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
+      int64_t roff = (int64_t)n * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
+#pragma unroll
+      for (int nr = 0; nr < NREP; ++nr) {
+        const int col = n0 + wn * WTN + nr * 16 + r16;
+        if (col >= p.Nout) continue;
+        float v = acc[m][nr][reg];
+        if (p.ws) {
+          atomicAdd(p.ws + (int64_t)row * p.Nout + col, v);
+        } else {
+          if (p.bias) v += p.bias[p.bias_mod ? col % p.bias_mod : col];
+          if (R) v += p.res_scale * ld_f(R + roff + col);
+          st_f(Y + yoff + col, act_apply(v, p.act, p.slope));
+        }
+      }
+    }
+  }
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs p) {
+  const int64_t total = (int64_t)p.M * p.Nout;
+  const int JHJW = p.JH * p.JW;
+  E* Y = reinterpret_cast<E*>(p.Y);
+  const E* R = reinterpret_cast<const E*>(p.R);
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int row = (int)(idx / p.Nout);
+    int col = (int)(idx - (int64_t)row * p.Nout);
+    int n = row / JHJW;
+    int rem = row - n * JHJW;
+    int j = rem / p.JW, i = rem - j * p.JW;
+    int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
+    float v = p.ws[idx];
+    if (p.bias) v += p.bias[p.bias_mod ? col % p.bias_mod : col];
+    if (R) v += p.res_scale * ld_f(R + (int64_t)n * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw + col);
+    st_f(Y + (int64_t)n * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw + col, act_apply(v, p.act, p.slope));
+  }
+}
+
+// tile configurations: {BM, BN, WM, WN}
+#define TPG_IGEMM_CFGS(X)   \
+  X(0, 128, 16, 4, 1)       \
+  X(1, 128, 32, 4, 1)       \
+  X(2, 128, 64, 2, 2)       \
+  X(3, 128, 96, 4, 1)       \
+  X(4, 128, 128, 2, 2)      \
+  X(5, 128, 224, 2, 2)
+
+int igemm_cfg_bn(int cfg) {
+#define X(id, bm, bn, wm, wn) if (cfg == id) return bn;
+  TPG_IGEMM_CFGS(X)
+#undef X
+  return -1;
+}
+int igemm_cfg_bm(int cfg) {
+#define X(id, bm, bn, wm, wn) if (cfg == id) return bm;
+  TPG_IGEMM_CFGS(X)
+#undef X
+  return -1;
+}
+
+int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s) {
+  const int bm = igemm_cfg_bm(cfg), bn = igemm_cfg_bn(cfg);
+  if (bm < 0) return -1;
+  dim3 grid((a.M + bm - 1) / bm, (a.Nout + bn - 1) / bn, a.ksplit);
+#define X(id, BM_, BN_, WM_, WN_)                                                              \
+  if (cfg == id) {                                                                             \
+    if (dtype == 1) hipLaunchKernelGGL((igemm_kernel<true, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_kernel<false, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);           \
+  }
+  TPG_IGEMM_CFGS(X)
+#undef X
+  return (int)hipGetLastError();
+}
+
+int launch_epilogue(const EpiArgs& a, hipStream_t s) {
+  int64_t total = (int64_t)a.M * a.Nout;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  if (blocks < 1) blocks = 1;
+  if (a.dtype == 1) hipLaunchKernelGGL(epilogue_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(epilogue_kernel<float>, dim3(blocks), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace tpg

@@ -1,0 +1,125 @@
+// Internal kernel interfaces of libtpgan_hip.so (gfx950).  The public C-ABI is
+// include/tpgan.h; tpg_capi.hip turns a tpg_conv_desc into the problems below.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define TPG_MAX_TAPS 64
+
+namespace tpg {
+
+// Fast unsigned division by a runtime constant for n, d < 2^31 (round-up method):
+// s = ceil(log2 d), mul = ceil(2^(31+s) / d) < 2^32, q = umulhi(n, mul) >> (s - 1).
+struct FastDiv {
+  uint32_t d, mul, shift;
+  __host__ void init(uint32_t div) {
+    d = div;
+    if (div <= 1) { d = 1; mul = 0; shift = 0; return; }
+    uint32_t s = 0;
+    while ((1u << s) < div) ++s;
+    mul = (uint32_t)(((1ull << (31 + s)) + div - 1) / div);
+    shift = s - 1;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return d == 1 ? n : (__umulhi(n, mul) >> shift);
+  }
+};
+
+// ---------------------------------------------------------------- implicit GEMM ----
+// Out[row][n'] = sum_{tap, c} A[pix(row, tap)][c] * Wp[n'][tap][c]   (+ epilogue)
+// row enumerates an output sub-grid (n, j, i): output pixel (oy0 + osy*j, ox0 + osx*i);
+// A pixel for tap t is (n, j*ist_h + dy[t], i*ist_w + dx[t]) (zero outside, or reflected).
+struct IgemmArgs {
+  const void* A;
+  int64_t a_sn, a_sh, a_sw;   // element strides; channel stride is 1
+  int A_H, A_W, C;            // A spatial bounds and real channels per tap
+  int upt;                    // 16-channel units per tap
+  int ntaps;
+  int nunits;                 // packed row length in units (multiple of units-per-k-tile)
+  int M, JH, JW;              // rows = N*JH*JW
+  int ist_h, ist_w;
+  int pad_mode;
+  int vec_ok;                 // A rows 16-byte aligned: vector loads allowed
+  const void* Wp;             // packed weights [Npad][nunits*16]
+  int Nout;                   // real n'
+  void* Y;
+  int64_t y_sn, y_sh, y_sw;   // channel stride 1
+  int oy0, ox0, osy, osx;
+  const float* bias;
+  int bias_mod;               // bias index = col % bias_mod when nonzero (composite n')
+  const void* R;
+  int64_t r_sn, r_sh, r_sw;
+  float res_scale;
+  int act;
+  float slope;
+  float* ws;                  // split-K fp32 accumulator [M][Nout]; null when ksplit == 1
+  int ksplit, kt_per_split;
+  FastDiv div_jw, div_jhjw;
+  int8_t dy[TPG_MAX_TAPS], dx[TPG_MAX_TAPS];
+};
+
+// ---------------------------------------------------------------- weight gradient ----
+// dW[a][b][r][s] += sum_p P[p][a] * Q[gather_t(p)][b]
+// p enumerates the P grid (n, py, px); gather_t(p) = (n, py*qst_h + dy[t], px*qst_w + dx[t]).
+struct WgradArgs {
+  const void* P;
+  int64_t p_sn, p_sh, p_sw;
+  int PH, PW, Ca;
+  const void* Q;
+  int64_t q_sn, q_sh, q_sw;
+  int QH, QW, Cb;             // Cb = b' extent (composite kh*kw*cb when bcomp)
+  int npix;                   // N*PH*PW
+  int qst_h, qst_w, pad_mode;
+  int vec_p, vec_q;
+  int ntaps;
+  int bcomp, comp_kw, comp_cb;  // b' = (r*kw + s)*cb + b when bcomp
+  float* dW;
+  int64_t w_sa, w_sb, w_sr, w_ss;
+  int ksplit, pix_per_split;
+  FastDiv div_pw, div_phpw;
+  int8_t dy[TPG_MAX_TAPS], dx[TPG_MAX_TAPS], tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
+};
+
+// ---------------------------------------------------------------- weight packing ----
+// Wp[n'][unit*16 + e] = W[a][b][r][s] (fp32 master -> compute dtype, zero padded).
+// n' and c' = (unit % upt)*16 + e decode by mode: 0 -> a, 1 -> b, 2 -> composite (r,s,b),
+// 3 -> composite (r,s,a); tap = unit / upt gives (r, s) when neither is composite.
+struct PackArgs {
+  const float* W;
+  int64_t w_sa, w_sb, w_sr, w_ss;
+  void* Wp;
+  int Npad, Nreal, nunits, upt, ntaps, Creal;
+  int nmode, cmode;
+  int comp_kw, comp_c;        // composite decode: idx = (r*kw + s)*comp_c + ch
+  int dtype;
+  int8_t tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
+};
+
+struct EpiArgs {               // split-K finalize
+  const float* ws;
+  int M, Nout, JH, JW;
+  void* Y;
+  int64_t y_sn, y_sh, y_sw;
+  int oy0, ox0, osy, osx;
+  const float* bias;
+  int bias_mod;
+  const void* R;
+  int64_t r_sn, r_sh, r_sw;
+  float res_scale;
+  int act;
+  float slope;
+  int dtype;
+};
+
+// launchers (return hipError_t as int); cfg selects the tile shape
+int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s);
+int igemm_cfg_bn(int cfg);
+int igemm_cfg_bm(int cfg);
+int launch_wgrad(const WgradArgs& a, int dtype, int cfg, hipStream_t s);
+int wgrad_cfg_bm(int cfg);
+int wgrad_cfg_bn(int cfg);
+int launch_pack(const PackArgs& a, hipStream_t s);
+int launch_epilogue(const EpiArgs& a, hipStream_t s);
+
+}  // namespace tpg

@@ -1,0 +1,115 @@
+"""ctypes binding of libtpgan_hip.so (C-ABI in include/tpgan.h).
+
+This is the boundary a maintainer of the reference would bind: plain
+pointers, strides and a hipStream_t, no torch types.  torch is used only to own device
+memory and to name the current HIP stream.
+
+The library is loaded lazily and loudly: there is no CPU fallback.  If the .so is
+missing, or no ROCm device is visible, every op raises RuntimeError.
+"""
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtpgan_hip.so")
+
+TPG_F32, TPG_BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+PAD_ZERO, PAD_REFLECT = 0, 1
+OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
+
+
+class TpgTensor(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("stride", ctypes.c_int64 * 4)]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n", "in_c", "in_h", "in_w", "out_c", "out_h", "out_w", "kh", "kw", "stride_h", "stride_w",
+        "pad_t", "pad_b", "pad_l", "pad_r", "pad_mode", "transposed", "dtype", "act")] + [
+        ("slope", ctypes.c_float), ("res_scale", ctypes.c_float), ("ksplit", ctypes.c_int32),
+        ("reserved", ctypes.c_int32)]
+
+
+EXPORTS = {
+    "tpg_conv2d_workspace": (ctypes.c_size_t, [ctypes.POINTER(ConvDesc), ctypes.c_int32]),
+    "tpg_conv2d_fwd": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, ctypes.c_void_p, TpgTensor,
+                                        TpgTensor, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "tpg_conv2d_bwd_data": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor,
+                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "tpg_conv2d_bwd_filter": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor,
+                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "tpg_act_bwd": (ctypes.c_int32, [ctypes.c_int32] * 5 + [ctypes.c_float, TpgTensor, TpgTensor, TpgTensor,
+                                                             ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_copy4d": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor, ctypes.c_void_p]),
+    "tpg_local_fuse_fwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [ctypes.POINTER(TpgTensor)] +
+                           [ctypes.POINTER(ctypes.c_int32)] * 4 + [TpgTensor, ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_local_fuse_bwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, ctypes.c_void_p,
+                                                                   ctypes.POINTER(TpgTensor)] +
+                           [ctypes.POINTER(ctypes.c_int32)] * 4 + [ctypes.c_void_p]),
+    "tpg_maxout2_fwd": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, TpgTensor, TpgTensor, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    "tpg_maxout2_bwd": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, TpgTensor, ctypes.c_void_p, TpgTensor,
+                                         ctypes.c_void_p]),
+    "tpg_adam": (ctypes.c_int32, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p] + [ctypes.c_float] * 5 + [ctypes.c_int32, ctypes.c_float,
+                                                                              ctypes.c_void_p]),
+    "tpg_version": (ctypes.c_char_p, []),
+    "tpg_last_error": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(require_gpu=True):
+    """Load libtpgan_hip.so (the HIP runtime it links is the one torch already loaded)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libtpgan_hip.so not built (%s): run `make -C tp-gan_amd` or "
+                           "__graft_entry__.build()" % LIB_PATH)
+    if require_gpu and not torch.cuda.is_available():
+        raise RuntimeError("tpgan HIP ops need a ROCm GPU; none is visible (there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError("tpgan HIP op failed (%d): %s" % (rc, _lib.tpg_last_error().decode()))
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return TPG_F32
+    if dt == torch.bfloat16:
+        return TPG_BF16
+    raise TypeError("tpgan ops support float32 and bfloat16, got %s" % dt)
+
+
+def tt(t):
+    """TpgTensor for a torch tensor of rank <= 4 (logical NCHW; missing dims get stride 0)."""
+    if t is None:
+        return TpgTensor()
+    if not t.is_cuda:
+        raise RuntimeError("tpgan ops need device tensors (got a %s tensor)" % t.device)
+    s = list(t.stride()) + [0] * (4 - t.dim())
+    d = TpgTensor()
+    d.data = t.data_ptr()
+    d.dtype = dtype_code(t.dtype)
+    for i in range(4):
+        d.stride[i] = s[i]
+    return d
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -1,0 +1,350 @@
+"""Autograd ops over libtpgan_hip.so — what the reference's torch.nn layers call into.
+
+Activation layout: every activation produced here is a logical NCHW tensor whose memory
+is channels-last with the pixel stride rounded up to 8 elements (16-byte rows for bf16),
+i.e. a channel slice of an [N, H, W, ceil8(C)] buffer.  Consumers accept any strides
+with channel stride 1; anything else (e.g. the user's NCHW fp32 images) is converted on
+the device by tpg_copy4d.
+
+Compute dtype: float32 by default (the reference's precision; MFMA f32 path), or
+bfloat16 inside `with compute_dtype(torch.bfloat16):` (MFMA bf16 path, fp32 accumulate).
+Master weights and their gradients stay float32.
+"""
+import contextlib
+import ctypes
+
+import torch
+
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, ConvDesc,
+                       TpgTensor, check, dtype_code, load, stream_ptr, tt)
+
+_DTYPE = [torch.float32]
+
+
+@contextlib.contextmanager
+def compute_dtype(dt):
+    _DTYPE.append(dt)
+    try:
+        yield
+    finally:
+        _DTYPE.pop()
+
+
+def get_compute_dtype():
+    return _DTYPE[-1]
+
+
+def _ceil8(c):
+    return (c + 7) // 8 * 8
+
+
+def new_act(n, c, h, w, dtype, device):
+    """Logical [n, c, h, w] view of a channels-last buffer with pixel stride ceil8(c)."""
+    buf = torch.empty((n, h, w, _ceil8(c)), dtype=dtype, device=device)
+    return buf.permute(0, 3, 1, 2)[:, :c]
+
+
+def is_cl(t):
+    return t.dim() == 4 and (t.stride(1) == 1 or t.shape[1] == 1)
+
+
+def to_cl(x, dtype):
+    """x as a channels-last activation of `dtype` (no copy when it already is one)."""
+    if x.dim() != 4:
+        raise ValueError("expected a 4-D tensor, got shape %s" % (tuple(x.shape),))
+    if x.dtype == dtype and x.stride(1) == 1:
+        return x
+    lib = load()
+    y = new_act(*x.shape, dtype=dtype, device=x.device)
+    n, c, h, w = x.shape
+    check(lib.tpg_copy4d(n, c, h, w, tt(x), tt(y), stream_ptr()))
+    return y
+
+
+def _fix_c1(t):
+    """A C == 1 tensor may report any channel stride; make it 1 for the kernels."""
+    if t.shape[1] == 1 and t.stride(1) != 1:
+        return t.as_strided(t.shape, (t.stride(0), 1, t.stride(2), t.stride(3)))
+    return t
+
+
+def act_code(act):
+    """(code, slope) for an activation module instance (or None)."""
+    if act is None:
+        return ACT_NONE, 0.0
+    if isinstance(act, torch.nn.LeakyReLU):
+        return ACT_LEAKY, float(act.negative_slope)
+    if isinstance(act, torch.nn.ReLU):
+        return ACT_RELU, 0.0
+    return None
+
+
+class ConvGeom:
+    """Static geometry of one Conv2d / ConvTranspose2d call."""
+
+    __slots__ = ("kh", "kw", "sh", "sw", "pt", "pb", "pl", "pr", "pad_mode", "transposed", "oph", "opw")
+
+    def __init__(self, kh, kw, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_ZERO, transposed=False,
+                 output_padding=(0, 0)):
+        self.kh, self.kw = kh, kw
+        self.sh, self.sw = stride
+        self.pt, self.pb, self.pl, self.pr = pad
+        self.pad_mode = pad_mode
+        self.transposed = transposed
+        self.oph, self.opw = output_padding
+
+    def out_hw(self, h, w):
+        if self.transposed:
+            return ((h - 1) * self.sh - self.pt - self.pb + self.kh + self.oph,
+                    (w - 1) * self.sw - self.pl - self.pr + self.kw + self.opw)
+        return ((h + self.pt + self.pb - self.kh) // self.sh + 1, (w + self.pl + self.pr - self.kw) // self.sw + 1)
+
+    def desc(self, n, cin, h, w, cout, oh, ow, dtype, act, slope, res_scale):
+        d = ConvDesc()
+        d.n, d.in_c, d.in_h, d.in_w = n, cin, h, w
+        d.out_c, d.out_h, d.out_w = cout, oh, ow
+        d.kh, d.kw, d.stride_h, d.stride_w = self.kh, self.kw, self.sh, self.sw
+        d.pad_t, d.pad_b, d.pad_l, d.pad_r = self.pt, self.pb, self.pl, self.pr
+        d.pad_mode = self.pad_mode
+        d.transposed = 1 if self.transposed else 0
+        d.dtype = dtype_code(dtype)
+        d.act = act
+        d.slope = slope
+        d.res_scale = res_scale
+        d.ksplit = 0
+        return d
+
+
+def _ws(lib, desc, op, device):
+    nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
+    if nb == 0:
+        check(-1)
+    return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+class _ConvAct(torch.autograd.Function):
+    """y = act(conv(x, w) + b [+ res_scale * residual]) with a HIP forward, input gradient,
+    weight gradient and a fused activation'/bias-gradient pass (backward reads only the
+    saved input and output, never the pre-activation)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale):
+        lib = load()
+        dtype = get_compute_dtype()
+        ctx.in_dtype = x.dtype
+        x = _fix_c1(to_cl(x, dtype))
+        n, cin, h, w = x.shape
+        if geom.transposed:
+            cin_w, cout = weight.shape[0], weight.shape[1]
+        else:
+            cout, cin_w = weight.shape[0], weight.shape[1]
+        if cin_w != cin:
+            raise RuntimeError("expected input with %d channels, got %d" % (cin_w, cin))
+        oh, ow = geom.out_hw(h, w)
+        y = new_act(n, cout, oh, ow, dtype, x.device)
+        res = None
+        if residual is not None:
+            res = _fix_c1(to_cl(residual, dtype))
+            if tuple(res.shape) != (n, cout, oh, ow):
+                raise RuntimeError("residual shape %s != output %s" % (tuple(res.shape), (n, cout, oh, ow)))
+        d = geom.desc(n, cin, h, w, cout, oh, ow, dtype, act, slope, res_scale)
+        ws = _ws(lib, d, OP_FWD, x.device)
+        wv = weight if weight.dtype == torch.float32 else weight.float()
+        check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bias.data_ptr() if bias is not None else None,
+                                 tt(res), tt(_fix_c1(y)), ws.data_ptr(), ws.numel(), stream_ptr()))
+        ctx.save_for_backward(x, weight, y)
+        ctx.geom, ctx.act, ctx.slope, ctx.res_scale = geom, act, slope, res_scale
+        ctx.has_bias, ctx.has_res = bias is not None, residual is not None
+        ctx.d = d
+        ctx.res_dtype = residual.dtype if residual is not None else None
+        ctx.x_dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        x, weight, y = ctx.saved_tensors
+        d = ctx.d
+        dtype = y.dtype
+        n, cout, oh, ow = y.shape
+        g = new_act(n, cout, oh, ow, dtype, y.device)
+        dbias = torch.zeros(cout, dtype=torch.float32, device=y.device) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        check(lib.tpg_act_bwd(n, cout, oh, ow, ctx.act, ctx.slope, tt(gy), tt(y), tt(_fix_c1(g)),
+                              dbias.data_ptr() if dbias is not None else None, stream_ptr()))
+        g = _fix_c1(g)
+        dx = dw = dres = None
+        wv = weight if weight.dtype == torch.float32 else weight.float()
+        if ctx.needs_input_grad[0]:
+            dx = new_act(*x.shape, dtype=dtype, device=x.device)
+            ws = _ws(lib, d, OP_BWD_DATA, x.device)
+            check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(_fix_c1(dx)), ws.data_ptr(), ws.numel(),
+                                          stream_ptr()))
+            if dx.dtype != ctx.in_dtype:
+                dx = dx.to(ctx.in_dtype)
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
+            if weight.dim() == 4:
+                dw = dw.contiguous(memory_format=torch.channels_last) if weight.is_contiguous(
+                    memory_format=torch.channels_last) else dw
+            dwv = dw if dw.dim() == 4 else dw.view(weight.shape[0], -1, d.kh, d.kw)
+            check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dwv), None, 0, stream_ptr()))
+            if dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
+        if ctx.has_res and ctx.needs_input_grad[3]:
+            dres = g if ctx.res_scale == 1.0 else g * ctx.res_scale
+            if dres.dtype != ctx.res_dtype:
+                dres = dres.to(ctx.res_dtype)
+        return dx, dw, dbias, dres, None, None, None, None
+
+
+def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_ZERO, act=None, residual=None,
+           res_scale=1.0, transposed=False, output_padding=(0, 0)):
+    """Functional entry: act is an activation module (LeakyReLU / ReLU) or None."""
+    code = act_code(act)
+    if code is None:
+        raise ValueError("activation %r cannot be fused" % (act,))
+    kh, kw = weight.shape[2], weight.shape[3]
+    geom = ConvGeom(kh, kw, stride, pad, pad_mode, transposed, output_padding)
+    return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale))
+
+
+def linear(x, weight, bias=None, act=None, image_hw=None):
+    """nn.Linear on [B, K] (or a [B, C, H, W] map flattened in NCHW order, fc1 at
+    D_and_G_model.py:289) as a full-kernel conv; returns [B, out]."""
+    out_f, in_f = weight.shape
+    if x.dim() == 4:
+        b, c, h, w = x.shape
+        w4 = weight.view(out_f, c, h, w)
+        y = conv2d(x, w4, bias, act=act)
+    else:
+        b = x.shape[0]
+        w4 = weight.view(out_f, in_f, 1, 1)
+        y = conv2d(x.reshape(b, in_f, 1, 1), w4, bias, act=act)
+    return y.reshape(b, out_f)
+
+
+class _Cat(torch.autograd.Function):
+    """torch.cat(dim=1) into one channels-last buffer; the backward is free channel views."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        lib = load()
+        dtype = get_compute_dtype()
+        n, _, h, w = xs[0].shape
+        ctot = sum(t.shape[1] for t in xs)
+        out = new_act(n, ctot, h, w, dtype, xs[0].device)
+        off = 0
+        sizes = []
+        for t in xs:
+            c = t.shape[1]
+            if t.shape[0] != n or t.shape[2] != h or t.shape[3] != w:
+                raise RuntimeError("Sizes of tensors must match except in dimension 1")
+            check(lib.tpg_copy4d(n, c, h, w, tt(t), tt(out[:, off:off + c]), stream_ptr()))
+            sizes.append(c)
+            off += c
+        ctx.sizes = sizes
+        ctx.dtypes = [t.dtype for t in xs]
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        outs = []
+        off = 0
+        for c, dt in zip(ctx.sizes, ctx.dtypes):
+            gv = gy[:, off:off + c]
+            outs.append(gv if gv.dtype == dt else gv.to(dt))
+            off += c
+        return tuple(outs)
+
+
+def cat(xs):
+    return _Cat.apply(*xs)
+
+
+class _LocalFuse(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, geom, *parts):
+        lib = load()
+        dtype = get_compute_dtype()
+        out_h, out_w, tops, lefts = geom
+        n, c = parts[0].shape[:2]
+        y = new_act(n, c, out_h, out_w, dtype, parts[0].device)
+        amax = torch.empty((n, out_h, out_w, c), dtype=torch.uint8, device=parts[0].device)
+        arr = (TpgTensor * 4)(*[tt(p) for p in parts])
+        ph = (ctypes.c_int32 * 4)(*[p.shape[2] for p in parts])
+        pw = (ctypes.c_int32 * 4)(*[p.shape[3] for p in parts])
+        top = (ctypes.c_int32 * 4)(*tops)
+        left = (ctypes.c_int32 * 4)(*lefts)
+        check(lib.tpg_local_fuse_fwd(n, c, out_h, out_w, arr, ph, pw, top, left, tt(_fix_c1(y)), amax.data_ptr(),
+                                     stream_ptr()))
+        ctx.save_for_backward(amax)
+        ctx.geom = geom
+        ctx.shapes = [tuple(p.shape) for p in parts]
+        ctx.dtypes = [p.dtype for p in parts]
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        (amax,) = ctx.saved_tensors
+        out_h, out_w, tops, lefts = ctx.geom
+        grads = []
+        tts = []
+        for i, (shp, dt) in enumerate(zip(ctx.shapes, ctx.dtypes)):
+            if ctx.needs_input_grad[1 + i]:
+                gdt = dt if dt in (torch.float32, torch.bfloat16) else torch.float32
+                gi = new_act(*shp, dtype=gdt, device=gy.device)
+                grads.append(gi)
+                tts.append(tt(_fix_c1(gi)))
+            else:
+                grads.append(None)
+                tts.append(TpgTensor())
+        if any(gr is not None for gr in grads):
+            n, c = ctx.shapes[0][:2]
+            arr = (TpgTensor * 4)(*tts)
+            ph = (ctypes.c_int32 * 4)(*[s[2] for s in ctx.shapes])
+            pw = (ctypes.c_int32 * 4)(*[s[3] for s in ctx.shapes])
+            check(lib.tpg_local_fuse_bwd(n, c, out_h, out_w, tt(gy), amax.data_ptr(), arr, ph, pw,
+                                         (ctypes.c_int32 * 4)(*tops), (ctypes.c_int32 * 4)(*lefts), stream_ptr()))
+        return (None,) + tuple(grads)
+
+
+def local_fuse(parts, out_hw, tops, lefts):
+    return _LocalFuse.apply((out_hw[0], out_hw[1], tuple(tops), tuple(lefts)), *parts)
+
+
+class _Maxout2(torch.autograd.Function):
+    """fc2: MaxPool1d(2, 2) over pairs of fc1 features (D_and_G_model.py:214,290)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        lib = load()
+        b, k = x.shape
+        m = k // 2
+        y = torch.empty((b, m), dtype=x.dtype, device=x.device)
+        amax = torch.empty((b, m), dtype=torch.uint8, device=x.device)
+        check(lib.tpg_maxout2_fwd(b, m, tt(x), tt(y), amax.data_ptr(), stream_ptr()))
+        ctx.save_for_backward(amax)
+        ctx.shape = (b, k)
+        ctx.dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        (amax,) = ctx.saved_tensors
+        b, k = ctx.shape
+        dx = torch.empty((b, k), dtype=ctx.dtype, device=gy.device)
+        check(lib.tpg_maxout2_bwd(b, k // 2, tt(gy), amax.data_ptr(), tt(dx), stream_ptr()))
+        return dx
+
+
+def maxout2(x):
+    return _Maxout2.apply(x)
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    """In-place Adam on flat fp32 buffers (torch.optim.Adam semantics)."""
+    lib = load()
+    check(lib.tpg_adam(param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                       lr, beta1, beta2, eps, weight_decay, step, grad_scale, stream_ptr()))
