@@ -1,0 +1,151 @@
+"""TP-GAN G+D train-step benchmark (BASELINE.json metric: faces/sec at 128x128, bs32/GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload = BASELINE.json configs[1]: full two-pathway Generator (global + 4 local
+pathways) + Discriminator train step, 128x128, bs32 per GPU, bf16 activations / MFMA
+with fp32 accumulate and fp32 master weights, synthetic Multi-PIE-shaped data resident in
+HBM, random-init weights.  Data parallel over N GPUs (one process per GPU, RCCL
+all-reduce of G and D gradients): per-GPU batch fixed, so scaling is weak.
+
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel (the 5x5 206->206
+enhance_features_128 convolution forward, timed with HIP events around its launches on
+the launching stream during the timed steps); `cpu_baseline` times the CPU oracle
+restatement (oracle/cpu_step.py, "port") on the host cores on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-iters", type=int, default=2)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.manual_seed(1234)
+
+    import D_and_G_model as DG
+    import tpgan_ops
+    import tpgan_train
+    from config import G as GCFG
+
+    G = DG.Generator(GCFG["zdim"], GCFG["num_classes"], use_batchnorm=False).to(dev)
+    D = DG.Discriminator().to(dev)
+    trainer = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16)
+    B = args.batch
+    batch = tpgan_train.synthetic_batch(B, dev, seed=1000 + rank)
+
+    # dominant kernel probe: enhance_features_128 (206 -> 206, 5x5, 128x128) forward
+    def match(d, which):
+        return which == "fwd" and d.in_c == 206 and d.out_c == 206 and d.kh == 5 and d.in_h == 128
+
+    for _ in range(args.warmup):
+        trainer.step(batch)
+    tpgan_ops.reset_flops()
+    trainer.step(batch)  # one counted step for the algorithmic FLOPs
+    flops_step = sum(tpgan_ops.FLOPS.values())
+    torch.cuda.synchronize()
+
+    tpgan_ops.PROBE["match"] = match
+    tpgan_ops.PROBE["events"] = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    tpgan_ops.PROBE["match"] = None
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    faces = world * B * args.steps / elapsed
+
+    evs = tpgan_ops.PROBE["events"]
+    k_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in evs) / max(len(evs), 1)
+    k_flops = evs[0][2] if evs else 0
+    achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        from oracle.cpu_step import time_cpu_step
+        fps, dt, thr = time_cpu_step(B=2, iters=args.cpu_iters, threads=args.cpu_threads)
+        cpu = {"value": round(fps, 4), "unit": "faces/s", "cores": thr, "kind": "port",
+               "sample": "oracle/cpu_step.py full G+D train step (no optimizer), B=2, %d timed steps after 1 warm-up, "
+                         "%.1f s/step, fp32 aten CPU" % (args.cpu_iters, dt)}
+
+    out = {
+        "metric": "faces/sec (G+D train step) at 128x128 bs32, 1/2/4/8 MI355X; % MFMA roofline",
+        "value": round(faces, 2),
+        "unit": "faces/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (U[-1,1] Multi-PIE-shaped batch resident in HBM; random-init weights)",
+        "config": {"workload": "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, "
+                               "128x128, bf16", "global_batch": B * world, "per_gpu_batch": B,
+                   "parallelism": "dp%d" % world},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "kernel": "tpg igemm fwd, enhance_features_128 (206->206, 5x5, 128x128, bs%d, +residual, "
+                               "LeakyReLU)" % B,
+                     "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4), "launches": len(evs)},
+        "step_mfma": {"algorithmic_tflop_per_step": round(flops_step / 1e12, 4),
+                      "gflop_per_face": round(flops_step / B / 1e9, 2),
+                      "achieved_tflops": round(flops_step / (ms_per_step * 1e-3) / 1e12, 2),
+                      "frac_of_peak": round(flops_step / (ms_per_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

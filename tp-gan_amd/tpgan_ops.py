@@ -20,6 +20,43 @@ from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, PAD_R
 
 _DTYPE = [torch.float32]
 
+# Algorithmic FLOPs (2 * MAC of every conv / conv-transpose / linear) issued since the
+# last reset, split by pass; bench.py divides by faces for the roofline figure.
+FLOPS = {"fwd": 0, "dgrad": 0, "wgrad": 0}
+
+
+def reset_flops():
+    for k in FLOPS:
+        FLOPS[k] = 0
+
+
+# Optional in-step timing probe for one conv shape (bench.py roofline): when
+# PROBE["match"](desc, pass) is true the HIP call is bracketed by HIP events on the
+# current stream (the stream the kernels are launched on).
+PROBE = {"match": None, "events": []}
+
+
+def _probe_begin(d, which):
+    m = PROBE["match"]
+    if m is None or not m(d, which):
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return e0
+
+
+def _probe_end(e0, d):
+    if e0 is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        PROBE["events"].append((e0, e1, _conv_flops(d)))
+
+
+def _conv_flops(d):
+    if d.transposed:
+        return 2 * d.n * d.in_h * d.in_w * d.in_c * d.out_c * d.kh * d.kw
+    return 2 * d.n * d.out_h * d.out_w * d.out_c * d.in_c * d.kh * d.kw
+
 
 @contextlib.contextmanager
 def compute_dtype(dt):
@@ -150,8 +187,11 @@ class _ConvAct(torch.autograd.Function):
         d = geom.desc(n, cin, h, w, cout, oh, ow, dtype, act, slope, res_scale)
         ws = _ws(lib, d, OP_FWD, x.device)
         wv = weight if weight.dtype == torch.float32 else weight.float()
+        FLOPS["fwd"] += _conv_flops(d)
+        e0 = _probe_begin(d, "fwd")
         check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bias.data_ptr() if bias is not None else None,
                                  tt(res), tt(_fix_c1(y)), ws.data_ptr(), ws.numel(), stream_ptr()))
+        _probe_end(e0, d)
         ctx.save_for_backward(x, weight, y)
         ctx.geom, ctx.act, ctx.slope, ctx.res_scale = geom, act, slope, res_scale
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
@@ -177,8 +217,11 @@ class _ConvAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = new_act(*x.shape, dtype=dtype, device=x.device)
             ws = _ws(lib, d, OP_BWD_DATA, x.device)
+            FLOPS["dgrad"] += _conv_flops(d)
+            e0 = _probe_begin(d, "dgrad")
             check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(_fix_c1(dx)), ws.data_ptr(), ws.numel(),
                                           stream_ptr()))
+            _probe_end(e0, d)
             if dx.dtype != ctx.in_dtype:
                 dx = dx.to(ctx.in_dtype)
         if ctx.needs_input_grad[1]:
@@ -187,7 +230,10 @@ class _ConvAct(torch.autograd.Function):
                 dw = dw.contiguous(memory_format=torch.channels_last) if weight.is_contiguous(
                     memory_format=torch.channels_last) else dw
             dwv = dw if dw.dim() == 4 else dw.view(weight.shape[0], -1, d.kh, d.kw)
+            FLOPS["wgrad"] += _conv_flops(d)
+            e0 = _probe_begin(d, "wgrad")
             check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dwv), None, 0, stream_ptr()))
+            _probe_end(e0, d)
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         if ctx.has_res and ctx.needs_input_grad[3]:

@@ -1,0 +1,161 @@
+"""The G+D train step of TP-GAN (build-defined: the reference has no GAN loop).
+
+The reference stops at the models (`D_and_G_model.py`) and the loss weights
+(`config.py:71-82`, marked provisional at :48); SURVEY.md §3C / §8f1 define the step this
+module implements:
+
+  1. G forward (Generator.forward, D_and_G_model.py:374-407)
+  2. D-step: D on [real ; fake.detach()] as one 2B batch, WGAN critic loss
+     mean D(fake) - mean D(real) (+ weight_gradient_penalty * GP when enabled), backward,
+     gradient all-reduce (data parallel), Adam
+  3. G-step: D frozen (UtilityMethods.set_requires_grad, :43-56), D(fake),
+     L = w_pix*L1(fake, frontal) + w_local*mean L1(local fakes, local targets)
+       + w_sym*L1(fake, mirror(fake)) - w_adv*mean D(fake) + w_tv*TV(fake)
+       + w_ce*CE(encoder_predict, label) [+ w_id*identity]
+     backward through D into G, gradient all-reduce, Adam
+  (config.loss weight_128 multiplies the 128-px pixel term; weight_64/weight_32 have no
+  producer because decoded_img32/64 are commented out in the reference, :254,:263.)
+
+Parameters of G and D live in one flat fp32 buffer each (params are views), so the
+optimizer is one HIP Adam launch per network and the data-parallel exchange is one
+RCCL all-reduce per network (torch.distributed, backend "nccl" = RCCL over xGMI).
+"""
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+import tpgan_ops
+from config import loss as LOSS_W
+from UtilityMethods import set_requires_grad
+
+
+class FlatParams:
+    """All parameters of `module` as views into one fp32 buffer, grads likewise."""
+
+    def __init__(self, module, device):
+        self.params = [p for p in module.parameters()]
+        total = sum(p.numel() for p in self.params)
+        self.data = torch.zeros(total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=device)
+        self.exp_avg = torch.zeros_like(self.data)
+        self.exp_avg_sq = torch.zeros_like(self.data)
+        self.step = 0
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            self._bind(p, off, n)
+            off += n
+
+    def _view(self, buf, p, off, n):
+        flat = buf[off:off + n]
+        if p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous():
+            a, b, h, w = p.shape
+            return flat.view(a, h, w, b).permute(0, 3, 1, 2)
+        return flat.view(p.shape)
+
+    def _bind(self, p, off, n):
+        v = self._view(self.data, p, off, n)
+        v.copy_(p.data)
+        p.data = v
+        p.grad = self._view(self.grad, p, off, n)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def adam(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0):
+        self.step += 1
+        tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
+                            weight_decay, self.step, grad_scale)
+
+
+def total_variation(x):
+    return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
+
+
+class TPGANTrainer:
+    """One process per GPU; call step(batch) with device-resident synthetic or real data.
+
+    batch keys: I128 (B,3,128,128) profile face, left_eye/right_eye (B,3,40,40),
+    nose (B,3,32,40), mouth (B,3,32,48), z (B,64), frontal (B,3,128,128) target,
+    frontal_left_eye/... local targets, label (B,) int64 identity.
+    """
+
+    def __init__(self, G, D, lr=1e-4, betas=(0.5, 0.999), compute_dtype=torch.bfloat16, loss_weights=None,
+                 gradient_penalty=False, process_group=None, identity_fn=None):
+        self.G, self.D = G, D
+        dev = next(G.parameters()).device
+        self.fG = FlatParams(G, dev)
+        self.fD = FlatParams(D, dev)
+        self.lr, self.betas = lr, betas
+        self.dtype = compute_dtype
+        self.w = dict(LOSS_W if loss_weights is None else loss_weights)
+        self.gp = gradient_penalty
+        if gradient_penalty:
+            raise NotImplementedError("WGAN-GP needs double backward through the HIP convs (next round)")
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.identity_fn = identity_fn
+        if self.world > 1:
+            dist.broadcast(self.fG.data, 0, group=process_group)
+            dist.broadcast(self.fD.data, 0, group=process_group)
+
+    def _allreduce(self, flat):
+        if self.world > 1:
+            dist.all_reduce(flat.grad, group=self.pg)
+
+    def step(self, b):
+        w = self.w
+        G, D = self.G, self.D
+        self.fG.zero_grad()
+        self.fD.zero_grad()
+        with tpgan_ops.compute_dtype(self.dtype):
+            outs = G(b["I128"], b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], True)
+            fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = outs
+            B = fake.shape[0]
+            # ---- D-step (critic on real and detached fake as one 2B batch)
+            real = tpgan_ops.to_cl(b["frontal"], self.dtype)
+            d_both = D(torch.cat([real, fake.detach()], 0)).float()
+            d_real, d_fake = d_both[:B], d_both[B:]
+            loss_D = d_fake.mean() - d_real.mean()
+            loss_D.backward()
+            self._allreduce(self.fD)
+            self.fD.adam(self.lr, self.betas, grad_scale=1.0 / self.world)
+            # ---- G-step through the frozen, updated D
+            set_requires_grad(D.parameters(), False)
+            d_gen = D(fake).float()
+            set_requires_grad(D.parameters(), True)
+        f32 = fake.float()
+        front = b["frontal"]
+        l_pix = w["weight_128"] * (f32 - front).abs().mean()
+        l_local = ((le_f.float() - b["frontal_left_eye"]).abs().mean() +
+                   (re_f.float() - b["frontal_right_eye"]).abs().mean() +
+                   (no_f.float() - b["frontal_nose"]).abs().mean() +
+                   (mo_f.float() - b["frontal_mouth"]).abs().mean()) / 4.0
+        l_sym = (f32 - f32.flip(3)).abs().mean()
+        l_adv = -d_gen.mean()
+        l_tv = total_variation(f32)
+        l_ce = F.cross_entropy(pred.float(), b["label"])
+        loss_G = (w["weight_pixelwise"] * l_pix + w["weight_pixelwise_local"] * l_local +
+                  w["weight_symmetry"] * l_sym + w["weight_adv_G"] * l_adv + w["weight_total_varation"] * l_tv +
+                  w["weight_cross_entropy"] * l_ce)
+        if self.identity_fn is not None:
+            loss_G = loss_G + w["weight_identity_preserving"] * self.identity_fn(f32, front)
+        loss_G.backward()
+        self._allreduce(self.fG)
+        self.fG.adam(self.lr, self.betas, grad_scale=1.0 / self.world)
+        return {"loss_D": loss_D.detach(), "loss_G": loss_G.detach()}
+
+
+def synthetic_batch(B, device, seed=0):
+    """Multi-PIE-shaped synthetic batch, U[-1, 1] images (DataAndDataset.py:220), z, labels."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+
+    def u(*s):
+        return (torch.rand(*s, generator=g) * 2 - 1).to(device)
+
+    b = {"I128": u(B, 3, 128, 128), "left_eye": u(B, 3, 40, 40), "right_eye": u(B, 3, 40, 40),
+         "nose": u(B, 3, 32, 40), "mouth": u(B, 3, 32, 48), "z": u(B, 64), "frontal": u(B, 3, 128, 128),
+         "frontal_left_eye": u(B, 3, 40, 40), "frontal_right_eye": u(B, 3, 40, 40), "frontal_nose": u(B, 3, 32, 40),
+         "frontal_mouth": u(B, 3, 32, 48),
+         "label": torch.randint(0, 347, (B,), generator=g).to(device)}
+    return b
