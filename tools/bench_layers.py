@@ -1,0 +1,104 @@
+"""Per-layer kernel timing (bf16) for the dominant TP-GAN conv shapes at bs32.
+
+    python tools/bench_layers.py [--iters 20] [--only NAME]
+
+For each shape: forward (act + optional residual), input gradient and weight gradient
+through the C-ABI, timed with HIP events on the launching stream, reported as
+algorithmic TFLOP/s and fraction of the 2.5 PF dense bf16 MFMA peak.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
+
+import torch  # noqa: E402
+
+import tpgan_ops as T  # noqa: E402
+from tpgan_lib import ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, check, load, stream_ptr, tt  # noqa: E402
+
+# name: (N, Cin, H, W, Cout, k, stride, pad, transposed, output_padding, act, residual)
+SHAPES = {
+    "enhance_128": (32, 206, 128, 128, 206, 5, 1, 2, False, 0, ACT_LEAKY, True),
+    "add_128": (32, 75, 128, 128, 75, 7, 1, 3, False, 0, ACT_LEAKY, True),
+    "conv0_res": (32, 64, 128, 128, 64, 7, 1, 3, False, 0, ACT_LEAKY, True),
+    "conv5_0": (32, 206, 128, 128, 64, 5, 1, 2, False, 0, ACT_LEAKY, False),
+    "enhance_64": (32, 208, 64, 64, 208, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "add_64": (32, 80, 64, 64, 80, 5, 1, 2, False, 0, ACT_LEAKY, True),
+    "enhance_32": (32, 416, 32, 32, 416, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "enhance_16": (32, 768, 16, 16, 768, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "up_128": (32, 208, 64, 64, 64, 3, 2, 1, True, 1, ACT_RELU, False),
+    "enh_8": (32, 576, 8, 8, 576, 2, 1, 0, False, 0, ACT_LEAKY, True),
+}
+
+
+def flops(s):
+    N, Cin, H, W, Cout, k, st, p, tr, op, act, res = s
+    if tr:
+        return 2 * N * H * W * Cin * Cout * k * k
+    OH = (H + 2 * p - k) // st + 1
+    OW = (W + 2 * p - k) // st + 1
+    return 2 * N * OH * OW * Cout * Cin * k * k
+
+
+def run(name, s, iters):
+    lib = load()
+    dev = torch.device("cuda", 0)
+    N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
+    dt = torch.bfloat16
+    geom = T.ConvGeom(k, k, (st, st), (p, p, p, p), 0, tr, (op, op))
+    OH, OW = geom.out_hw(H, W)
+    x = T.new_act(N, Cin, H, W, dt, dev)
+    x.normal_()
+    w = torch.randn((Cin, Cout, k, k) if tr else (Cout, Cin, k, k), device=dev) * 0.05
+    w = w.contiguous(memory_format=torch.channels_last)
+    b = torch.zeros(Cout, device=dev)
+    y = T.new_act(N, Cout, OH, OW, dt, dev)
+    res = T.new_act(N, Cout, OH, OW, dt, dev).normal_() if use_res else None
+    g = T.new_act(N, Cout, OH, OW, dt, dev).normal_()
+    dx = T.new_act(N, Cin, H, W, dt, dev)
+    dw = torch.zeros_like(w)
+    d = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
+    wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
+    wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
+    calls = {
+        "fwd": lambda: check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w), b.data_ptr(), tt(res), tt(y),
+                                                wsf.data_ptr(), wsf.numel(), stream_ptr())),
+        "dgrad": lambda: check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w), tt(dx), wsd.data_ptr(),
+                                                       wsd.numel(), stream_ptr())),
+        "wgrad": lambda: check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0,
+                                                         stream_ptr())),
+    }
+    f = flops(s)
+    out = []
+    for kind, fn in calls.items():
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        tf = f / (ms * 1e-3) / 1e12
+        out.append("%s %.3f ms %.0f TF/s (%.1f%%)" % (kind, ms, tf, 100 * tf / 2500))
+    print("%-12s %6.1f GF | %s" % (name, f / 1e9, " | ".join(out)), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    for name, s in SHAPES.items():
+        if a.only and name not in a.only.split(","):
+            continue
+        run(name, s, a.iters)
+
+
+if __name__ == "__main__":
+    main()

@@ -68,6 +68,10 @@ struct Prob {
   PackArgs pk;
   int cfg = 0;
   size_t wp_bytes = 0, sk_bytes = 0;
+  bool halo = false;          // run on the halo-tiled direct-conv kernel
+  HaloArgs h;
+  int hcfg = -1;
+  size_t g_wp = 0, g_sk = 0;  // generic-kernel sizes, kept for the run-time fallback
 };
 
 static int choose_cfg(int nout) {
@@ -199,6 +203,51 @@ static int32_t check_desc(const tpg_conv_desc* d) {
   return 0;
 }
 
+// Route a unit-stride (sub-)grid problem to the halo kernel when it is big enough.
+static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
+  IgemmArgs& a = P.a;
+  if (!unit_stride || a.ntaps < 1 || a.C < 1) return;
+  if (a.JW < 16 || (int64_t)a.JH * a.JW < 1024) return;
+  int dymin = 127, dymax = -128, dxmin = 127, dxmax = -128;
+  for (int t = 0; t < a.ntaps; ++t) {
+    dymin = std::min<int>(dymin, a.dy[t]); dymax = std::max<int>(dymax, a.dy[t]);
+    dxmin = std::min<int>(dxmin, a.dx[t]); dxmax = std::max<int>(dxmax, a.dx[t]);
+  }
+  if (dymax - dymin > 6 || dxmax - dxmin > 6) return;
+  // tile width: the one wasting fewer columns (ties -> 32, smaller halo overhead)
+  const int w32 = cdiv(a.JW, 32) * 32, w16 = cdiv(a.JW, 16) * 16;
+  const int tw = (w32 <= w16) ? 32 : 16, th = 256 / tw;
+  int bn;
+  if (a.Nout <= 32) bn = 32;
+  else if (a.Nout <= 64) bn = 64;
+  else if (a.Nout <= 96) bn = 96;
+  else if (a.Nout <= 128) bn = 128;
+  else if (a.Nout <= 224) bn = a.Nout > 192 ? 224 : 128;
+  else bn = (cdiv(a.Nout, 224) * 224 < cdiv(a.Nout, 128) * 128) ? 224 : 128;
+  const int cfg = halo_cfg(tw, std::max(dymax - dymin, dxmax - dxmin) + 1, bn);
+  if (cfg < 0) return;
+  HaloArgs& h = P.h;
+  memset(&h, 0, sizeof(h));
+  const int ks_elems = dtype == TPG_BF16 ? 32 : 16;
+  h.A_H = a.A_H; h.A_W = a.A_W; h.C = a.C;
+  h.nks = cdiv(a.C, ks_elems);
+  h.ntaps = a.ntaps;
+  h.dymin = dymin; h.dxmin = dxmin;
+  h.HH = th + dymax - dymin; h.HW = tw + dxmax - dxmin;
+  for (int t = 0; t < a.ntaps; ++t) h.toff[t] = (a.dy[t] - dymin) * h.HW + (a.dx[t] - dxmin);
+  h.pad_mode = a.pad_mode;
+  h.N = N; h.JH = a.JH; h.JW = a.JW;
+  h.tiles_h = cdiv(a.JH, th); h.tiles_w = cdiv(a.JW, tw);
+  h.BN = bn; h.ntiles = cdiv(a.Nout, bn); h.Nout = a.Nout;
+  h.oy0 = a.oy0; h.ox0 = a.ox0; h.osy = a.osy; h.osx = a.osx;
+  P.halo = true;
+  P.hcfg = cfg;
+  P.g_wp = P.wp_bytes;
+  P.g_sk = P.sk_bytes;
+  P.wp_bytes = (size_t)rup((int64_t)halo_wp_bytes(h.nks, h.ntaps, bn, h.ntiles), 256);
+  P.sk_bytes = 0;
+}
+
 // ---- forward plans
 static std::vector<Prob> plan_fwd(const tpg_conv_desc* d, bool composite) {
   std::vector<Prob> v;
@@ -217,6 +266,7 @@ static std::vector<Prob> plan_fwd(const tpg_conv_desc* d, bool composite) {
       P.a.pad_mode = d->pad_mode;
       P.pk.nmode = 0; P.pk.cmode = 1;
       finish(P, d->dtype, d->n * d->out_h * d->out_w);
+      maybe_halo(P, d->dtype, d->n, d->stride_h == 1 && d->stride_w == 1);
       v.push_back(P);
     }
   } else {
@@ -232,6 +282,7 @@ static std::vector<Prob> plan_fwd(const tpg_conv_desc* d, bool composite) {
         P.a.C = d->in_c; P.a.A_H = d->in_h; P.a.A_W = d->in_w; P.a.Nout = d->out_c;
         P.pk.nmode = 1; P.pk.cmode = 0;
         finish(P, d->dtype, d->n * P.a.JH * P.a.JW);
+        maybe_halo(P, d->dtype, d->n, true);
         v.push_back(P);
       }
     }
@@ -272,6 +323,7 @@ static std::vector<Prob> plan_bwd_data(const tpg_conv_desc* d, bool composite) {
         P.a.C = d->out_c; P.a.A_H = d->out_h; P.a.A_W = d->out_w; P.a.Nout = d->in_c;
         P.pk.nmode = 1; P.pk.cmode = 0;
         finish(P, d->dtype, d->n * P.a.JH * P.a.JW);
+        maybe_halo(P, d->dtype, d->n, true);
         v.push_back(P);
       }
     }
@@ -288,6 +340,7 @@ static std::vector<Prob> plan_bwd_data(const tpg_conv_desc* d, bool composite) {
       P.a.C = d->out_c; P.a.A_H = d->out_h; P.a.A_W = d->out_w; P.a.Nout = d->in_c;
       P.pk.nmode = 0; P.pk.cmode = 1;
       finish(P, d->dtype, d->n * d->in_h * d->in_w);
+      maybe_halo(P, d->dtype, d->n, d->stride_h == 1 && d->stride_w == 1);
       v.push_back(P);
     }
   }
@@ -309,7 +362,10 @@ static bool bwd_data_composite(const tpg_conv_desc* d, const tpg_tensor* g, cons
 
 static size_t probs_ws(const std::vector<Prob>& v) {
   size_t wp = 0, sk = 0;
-  for (const Prob& P : v) { wp += P.wp_bytes; sk = std::max(sk, P.sk_bytes); }
+  for (const Prob& P : v) {
+    wp += std::max(P.wp_bytes, P.g_wp);
+    sk = std::max(sk, std::max(P.sk_bytes, P.g_sk));
+  }
   return wp + sk;
 }
 
@@ -341,9 +397,16 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
   size_t need = probs_ws(v);
   if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
   const bool vA = vec_ok(A, dtype);
+  if (!vA)  // the halo kernel only takes 16-byte aligned channels-last rows
+    for (Prob& P : v)
+      if (P.halo) {
+        P.halo = false;
+        P.wp_bytes = P.g_wp;
+        P.sk_bytes = P.g_sk;
+      }
   size_t off = 0;
   std::vector<char*> wps;
-  for (Prob& P : v) { wps.push_back(ws + off); off += P.wp_bytes; }
+  for (Prob& P : v) { wps.push_back(ws + off); off += std::max(P.wp_bytes, P.g_wp); }
   char* sk = ws + off;
   for (size_t i = 0; i < v.size(); ++i) {
     Prob& P = v[i];
@@ -352,6 +415,23 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     k.W = reinterpret_cast<const float*>(W.data);
     k.w_sa = W.stride[0]; k.w_sb = W.stride[1]; k.w_sr = W.stride[2]; k.w_ss = W.stride[3];
     k.Wp = wps[i];
+    if (P.halo) {
+      HaloArgs& h = P.h;
+      if (h.ntaps > 0) {
+        int e = launch_pack_halo(k, h.nks, h.BN, h.ntiles, s);
+        if (e) return hip_check(e, "pack_halo");
+      }
+      h.A = A.data; h.a_sn = A.stride[0]; h.a_sh = A.stride[2]; h.a_sw = A.stride[3];
+      h.vec_ok = vA;
+      h.Wp = wps[i];
+      h.Y = Y.data; h.y_sn = Y.stride[0]; h.y_sh = Y.stride[2]; h.y_sw = Y.stride[3];
+      h.bias = bias;
+      h.R = R.data; h.r_sn = R.stride[0]; h.r_sh = R.stride[2]; h.r_sw = R.stride[3];
+      h.res_scale = res_scale; h.act = act; h.slope = slope;
+      int e = launch_halo(h, dtype, P.hcfg, s);
+      if (e) return hip_check(e, "halo conv");
+      continue;
+    }
     if (a.nunits > 0) {
       int e = launch_pack(k, s);
       if (e) return hip_check(e, "pack");

@@ -1,0 +1,355 @@
+// Halo-tiled direct convolution for gfx950 — the stride-1 / sub-pixel hot path.
+//
+// Covers every conv whose taps read the A grid with unit stride: Conv2d forward at
+// stride 1 (all 3x3 / 5x5 / 7x7 / 2x2-reflect layers of G and D), the Conv2d input
+// gradient at any stride and the ConvTranspose2d forward (one launch per parity class,
+// SURVEY.md §7 step 5).  That is > 90 % of the G+D train-step MACs of the fwd + dgrad passes.
+//
+// Block = a TH x TW tile of output (sub-grid) pixels of one image x BN output channels,
+// 8 waves.  K loop: for each 64-byte channel step (bf16: 32 ch, f32: 16 ch)
+//   - the input halo (TH + dy range) x (TW + dx range) pixels x 64 B is gathered ONCE
+//     into LDS (zero / reflected outside the image) and reused by all taps;
+//   - for each tap the [BN][64 B] weight slice (packed contiguous, pre-swizzled) is staged
+//     through a second LDS double buffer, and every wave runs MREP x NREP MFMAs with A
+//     fragments read from the halo at the tap's (dy, dx) shift.
+// Next step's halo and next tap's weights are prefetched into registers while the current
+// tap computes (software pipeline, one barrier per tap).
+//
+// LDS images use 64-byte pixel rows; the 16-byte chunk g of row p is stored at
+// g ^ (((p >> 2) & 1) << 1), which makes the ds_read_b128 fragment reads of both
+// operands bank-conflict free for any shift (checked exhaustively over the gfx950
+// ds_read_b128 lane groups).
+#include "tpg_internal.h"
+#include <type_traits>
+
+namespace tpg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+__device__ __forceinline__ int hswz(int row) { return ((row >> 2) & 1) << 1; }
+
+__host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 128; }
+
+// mask_chunk on a native 4 x u32 vector (first-class value: stays in VGPRs)
+template <int EPC>
+__device__ __forceinline__ u32x4 mask_chunk4(u32x4 v, int c0, int C) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if constexpr (EPC == 8) {
+      const int e = c0 + 2 * d;
+      v[d] &= (e + 1 < C) ? 0xFFFFFFFFu : ((e < C) ? 0x0000FFFFu : 0u);
+    } else {
+      v[d] = (c0 + d < C) ? v[d] : 0u;
+    }
+  }
+  return v;
+}
+
+__device__ __forceinline__ float h_act(float v, int act, float slope) {
+  if (act == 2) return v > 0.f ? v : v * slope;
+  if (act == 1) return v > 0.f ? v : 0.f;
+  return v;
+}
+
+__device__ __forceinline__ int h_refl(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+template <bool BF, int TH, int TW, int KMAX, int BN, int WM, int WN>
+__global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
+  using E = typename std::conditional<BF, __bf16, float>::type;
+  constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
+  constexpr int KS = 4 * EPC;                // channels per 64-byte step
+  constexpr int BM = TH * TW;
+  constexpr int HMAX = (TH + KMAX - 1) * (TW + KMAX - 1);  // halo pixels for KMAX x KMAX taps
+  constexpr int HL = (HMAX * 4 + 511) / 512; // halo chunks staged per thread
+  constexpr int BNL = halo_bnl(BN);          // weight rows per LDS slot (multiple of 128)
+  constexpr int GL = BNL / 128;              // 1 KiB LDS-DMA pieces per wave per step
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MREP = WTM / 16, NREP = WTN / 16;
+  static_assert(WM * WN == 8, "8 waves");
+  static_assert(MREP * 16 * WM == BM && NREP * 16 * WN == BN, "tile");
+  static_assert(TW % 16 == 0, "tile rows must hold whole 16-pixel fragments");
+
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  u32x4* halo = lds;                                   // [2][HMAX][4]
+  u32x4* wts = lds + 2 * HMAX * 4;                     // [3][BNL][4] ring
+  int* s_toff = reinterpret_cast<int*>(wts + 3 * BNL * 4);  // [TPG_MAX_TAPS]
+
+  const int tid = threadIdx.x;
+  if (tid < TPG_MAX_TAPS) s_toff[tid] = p.toff[tid];
+  const int HW = p.HW, HP = p.HH * HW;
+  const int tiles = p.tiles_h * p.tiles_w;
+  const int nimg = blockIdx.x / tiles;
+  const int trem = blockIdx.x - nimg * tiles;
+  const int th = trem / p.tiles_w;
+  const int j0 = th * TH, i0 = (trem - th * p.tiles_w) * TW;
+  const int n0 = blockIdx.y * BN;
+  const E* Ag = reinterpret_cast<const E*>(p.A) + (int64_t)nimg * p.a_sn;
+  const int wave = tid >> 6, lane = tid & 63;
+  // packed weights: Wp[step][ntile][BNL][4 chunks]; this wave streams GL KiB of each slice
+  const char* wsrc = reinterpret_cast<const char*>(p.Wp) + (int64_t)blockIdx.y * BNL * 64 +
+                     (wave * GL * 1024 + lane * 16);
+  const int64_t wstep = (int64_t)p.ntiles * BNL * 64;
+
+  // ---- per-thread halo slots (fixed across k-steps): element offset inside the image
+  // (negative = outside -> zero)
+  int hoff[HL];
+#pragma unroll
+  for (int q = 0; q < HL; ++q) {
+    const int idx = tid + 512 * q;
+    const int hp = idx >> 2, ch = idx & 3;
+    hoff[q] = -1;
+    if (hp < HP) {
+      const int hy = hp / HW, hx = hp - (hp / HW) * HW;
+      int gy = j0 + p.dymin + hy, gx = i0 + p.dxmin + hx;
+      if (p.pad_mode) { gy = h_refl(gy, p.A_H); gx = h_refl(gx, p.A_W); }
+      if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W)
+        hoff[q] = gy * (int)p.a_sh + gx * (int)p.a_sw + ch * EPC;
+    }
+  }
+
+  // Halo chunks are loaded raw (clamped address, unconditional 16-byte load) and masked
+  // only when written to LDS a whole k-step later.  (vec-only kernel: the planner sends
+  // unaligned tensors to the generic kernel.)
+  u32x4 hreg[HL];
+  int hc = 0;
+  auto load_halo = [&](int ks) {
+    const int cbase = ks * KS;
+    hc = cbase + (tid & 3) * EPC;
+#pragma unroll
+    for (int q = 0; q < HL; ++q) {
+      const bool ok = hoff[q] >= 0 && hc < p.C;
+      hreg[q] = *reinterpret_cast<const u32x4*>(Ag + (ok ? hoff[q] + cbase : 0));
+    }
+  };
+  auto store_halo = [&](int buf) {
+    u32x4* H = halo + buf * HMAX * 4;
+#pragma unroll
+    for (int q = 0; q < HL; ++q) {
+      const int idx = tid + 512 * q;
+      const int hp = idx >> 2;
+      u32x4 v = mask_chunk4<EPC>(hreg[q], hc, p.C);
+      if (hoff[q] < 0) v = u32x4{0u, 0u, 0u, 0u};
+      if (hp < HP) H[hp * 4 + ((idx & 3) ^ hswz(hp))] = v;
+    }
+  };
+  // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
+  auto issue_w = [&](int step, int slot) {
+    const char* src = wsrc + (int64_t)step * wstep;
+    char* dst = reinterpret_cast<char*>(wts + slot * BNL * 4) + wave * GL * 1024;
+#pragma unroll
+    for (int j = 0; j < GL; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, 0, 0);
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int l16 = lane & 15, g = lane >> 4;
+  int hbase[MREP];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m) {
+    const int q = wm * WTM + m * 16 + l16;
+    const int ty = q / TW, tx = q - (q / TW) * TW;
+    hbase[m] = ty * HW + tx;
+  }
+  f32x4 acc[MREP][NREP];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m)
+#pragma unroll
+    for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int hbuf, int wslot, int toff) {
+    const u32x4* H = halo + hbuf * HMAX * 4;
+    const u32x4* Wl = wts + wslot * BNL * 4;
+    u32x4 af[MREP];
+#pragma unroll
+    for (int m = 0; m < MREP; ++m) {
+      const int hp = hbase[m] + toff;
+      af[m] = H[hp * 4 + (g ^ hswz(hp))];
+    }
+#pragma unroll
+    for (int n = 0; n < NREP; ++n) {
+      const int r = wn * WTN + n * 16 + l16;
+      const u32x4 bv = Wl[r * 4 + (g ^ hswz(r))];
+#pragma unroll
+      for (int m = 0; m < MREP; ++m) {
+        if constexpr (BF) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[m]),
+                                                              __builtin_bit_cast(bf16x8, bv), acc[m][n], 0, 0, 0);
+        } else {
+          const f32x4 a4 = __builtin_bit_cast(f32x4, af[m]);
+          const f32x4 b4 = __builtin_bit_cast(f32x4, bv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], acc[m][n], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // Software pipeline over steps s = ks*ntaps + t, one barrier per step:
+  //   start of s : LDS-DMA of step s+2's weights into ring slot (s+2)%3 (unconditional,
+  //                clamped, so every wave always has GL DMA pieces per step in flight);
+  //                at t == 0 the halo of k-step ks+1 into registers
+  //   body       : MFMAs on ring slot s%3 and halo buffer ks&1
+  //   end of s   : at t == ntaps-1 write the next halo to LDS; s_waitcnt vmcnt(GL)
+  //                retires step s+1's DMA (issued during s-1) while step s+2's stays in
+  //                flight; lgkmcnt(0); s_barrier.  Step s+1 then reads what was retired.
+  const int nks = p.nks, ntaps = p.ntaps;
+  const int total = nks * ntaps;
+  __syncthreads();  // tap table
+  if (total > 0) {
+    load_halo(0);
+    issue_w(0, 0);
+    issue_w(min(1, total - 1), 1);
+    store_halo(0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    int ks = 0, t = 0, slot = 0;
+    int toff = s_toff[0];
+    for (int s = 0; s < total; ++s) {
+      const bool more_ks = ks + 1 < nks;
+      if (t == 0 && more_ks) load_halo(ks + 1);
+      const int slot2 = slot == 0 ? 2 : slot - 1;  // (s + 2) % 3
+      issue_w(min(s + 2, total - 1), slot2);
+      const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];  // read ahead of its use
+      compute(ks & 1, slot, toff);
+      toff = toff_next;
+      if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
+      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      slot = slot == 2 ? 0 : slot + 1;
+      if (++t == ntaps) { t = 0; ++ks; }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
+  }
+
+  // ---- epilogue
+  E* Y = reinterpret_cast<E*>(p.Y);
+  const E* R = reinterpret_cast<const E*>(p.R);
+#pragma unroll
+  for (int m = 0; m < MREP; ++m) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int q = wm * WTM + m * 16 + 4 * g + reg;
+      const int ty = q / TW, tx = q - (q / TW) * TW;
+      const int j = j0 + ty, i = i0 + tx;
+      if (j >= p.JH || i >= p.JW) continue;
+      const int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
+      const int64_t yoff = (int64_t)nimg * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
+      const int64_t roff = (int64_t)nimg * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
+#pragma unroll
+      for (int nr = 0; nr < NREP; ++nr) {
+        const int col = n0 + wn * WTN + nr * 16 + l16;
+        if (col >= p.Nout) continue;
+        float v = acc[m][nr][reg];
+        if (p.bias) v += p.bias[col];
+        if (R) v += p.res_scale * (float)R[roff + col];
+        Y[yoff + col] = (E)h_act(v, p.act, p.slope);
+      }
+    }
+  }
+}
+
+// {id, TH, TW, KMAX, BN, WM, WN}; id = 15 * (TW == 16) + 5 * kclass + bn index
+#define TPG_HALO_BN(X, ID, TH, TW, K)  \
+  X(ID + 0, TH, TW, K, 32, 8, 1)       \
+  X(ID + 1, TH, TW, K, 64, 8, 1)       \
+  X(ID + 2, TH, TW, K, 96, 8, 1)       \
+  X(ID + 3, TH, TW, K, 128, 4, 2)      \
+  X(ID + 4, TH, TW, K, 224, 4, 2)
+#define TPG_HALO_CFGS(X)               \
+  TPG_HALO_BN(X, 0, 8, 32, 3)          \
+  TPG_HALO_BN(X, 5, 8, 32, 5)          \
+  TPG_HALO_BN(X, 10, 8, 32, 7)         \
+  TPG_HALO_BN(X, 15, 16, 16, 3)        \
+  TPG_HALO_BN(X, 20, 16, 16, 5)        \
+  TPG_HALO_BN(X, 25, 16, 16, 7)
+
+int halo_cfg(int tw, int kspan, int bn) {
+  const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : -1;
+  if (bi < 0 || kspan > 7 || (tw != 16 && tw != 32)) return -1;
+  const int kc = kspan <= 3 ? 0 : kspan <= 5 ? 1 : 2;
+  return (tw == 16 ? 15 : 0) + 5 * kc + bi;
+}
+
+static size_t halo_lds_bytes(int th, int tw, int k, int bn) {
+  return (size_t)(2 * (th + k - 1) * (tw + k - 1) * 4 + 3 * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
+}
+
+int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s) {
+  dim3 grid(a.N * a.tiles_h * a.tiles_w, a.ntiles);
+#define X(id, TH_, TW_, K_, BN_, WM_, WN_)                                                                    \
+  if (cfg == (id)) {                                                                                          \
+    const size_t lds = halo_lds_bytes(TH_, TW_, K_, BN_);                                                     \
+    if (dtype == 1) {                                                                                         \
+      auto k = halo_kernel<true, TH_, TW_, K_, BN_, WM_, WN_>;                                                \
+      static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                    (int)lds), true);                                         \
+      (void)once;                                                                                             \
+      hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                      \
+    } else {                                                                                                  \
+      auto k = halo_kernel<false, TH_, TW_, K_, BN_, WM_, WN_>;                                               \
+      static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                    (int)lds), true);                                         \
+      (void)once;                                                                                             \
+      hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                      \
+    }                                                                                                         \
+    return (int)hipGetLastError();                                                                            \
+  }
+  TPG_HALO_CFGS(X)
+#undef X
+  return -1;
+}
+
+// -------------------------------------------------------------- halo weight packing --
+// Wp[ks*ntaps + tap][ntile][BNL rows][4 chunks][EPC]: row r of N-tile nt is output
+// n' = nt*BN + r (zero when r >= BN or n' >= Nout); chunk' = chunk ^ hswz(r) holds
+// logical channels c = ks*KS + chunk*EPC + e of that tap.
+__global__ __launch_bounds__(256) void pack_halo_kernel(const PackArgs p, int nks, int bn, int bnl, int ntiles) {
+  const int epc = p.dtype == 1 ? 8 : 4;
+  const int row = 4 * epc;  // elements per 64-byte row
+  const int64_t total = (int64_t)nks * p.ntaps * ntiles * bnl * row;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t rr = idx / row;
+    const int inrow = (int)(idx - rr * row);
+    const int r = (int)(rr % bnl);
+    rr /= bnl;
+    const int nt = (int)(rr % ntiles);
+    rr /= ntiles;
+    const int tap = (int)(rr % p.ntaps);
+    const int ks = (int)(rr / p.ntaps);
+    const int pchunk = inrow / epc, e = inrow - pchunk * epc;
+    const int chunk = pchunk ^ hswz(r);
+    const int c = ks * row + chunk * epc + e;
+    const int np = nt * bn + r;
+    float v = 0.f;
+    if (r < bn && np < p.Nreal && c < p.Creal) {
+      int a = 0, b = 0;
+      const int tr = p.tr[tap], ts = p.ts[tap];
+      if (p.nmode == 0) a = np; else b = np;
+      if (p.cmode == 0) a = c; else b = c;
+      v = p.W[a * p.w_sa + b * p.w_sb + tr * p.w_sr + ts * p.w_ss];
+    }
+    if (p.dtype == 1) reinterpret_cast<__bf16*>(p.Wp)[idx] = (__bf16)v;
+    else reinterpret_cast<float*>(p.Wp)[idx] = v;
+  }
+}
+
+size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles) {
+  return (size_t)nks * ntaps * ntiles * halo_bnl(bn) * 64;
+}
+
+int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s) {
+  const int64_t total = (int64_t)nks * a.ntaps * ntiles * halo_bnl(bn) * (a.dtype == 1 ? 32 : 16);
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(pack_halo_kernel, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles);
+  return (int)hipGetLastError();
+}
+
+}  // namespace tpg

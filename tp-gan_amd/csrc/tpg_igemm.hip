@@ -102,6 +102,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
   const int64_t wrow = (int64_t)p.nunits * 16;
 
   uint4 ra[RA], rb[RB];
+  int a_c = 0;
+  uint32_t a_ok = 0;
   int tap = 0, cu = 0;
   {
     int u = kt0 * UPK + slot;
@@ -115,24 +117,25 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
     const bool tap_ok = tap < p.ntaps;
     const int dy = tap_ok ? s_dy[tap] : 0;
     const int dx = tap_ok ? s_dx[tap] : 0;
+    a_c = c;
+    a_ok = 0;
 #pragma unroll
     for (int q = 0; q < RA; ++q) {
       int iy = by[q] + dy, ix = bx[q] + dx;
       if (p.pad_mode) { iy = reflect_idx(iy, p.A_H); ix = reflect_idx(ix, p.A_W); }
-      bool ok = tap_ok && rv[q] && (unsigned)iy < (unsigned)p.A_H && (unsigned)ix < (unsigned)p.A_W && c < p.C;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) {
-        const E* src = Ag + a_base[q] + (int64_t)iy * p.a_sh + (int64_t)ix * p.a_sw + c;
-        if (p.vec_ok && c + EPC <= p.C) {
-          v = *reinterpret_cast<const uint4*>(src);
-        } else {
-          union { uint4 u; E e[EPC]; } t;
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) t.e[e] = (c + e < p.C) ? src[e] : (E)0.f;
-          v = t.u;
-        }
+      const bool ok = tap_ok && rv[q] && (unsigned)iy < (unsigned)p.A_H && (unsigned)ix < (unsigned)p.A_W && c < p.C;
+      const int64_t off = a_base[q] + (int64_t)iy * p.a_sh + (int64_t)ix * p.a_sw + c;
+      a_ok |= (ok ? 1u : 0u) << q;
+      if (p.vec_ok) {
+        ra[q] = *reinterpret_cast<const uint4*>(Ag + (ok ? off : 0));  // masked at store time
+      } else {
+        union { uint4 u; E e[EPC]; } t;
+        t.u = make_uint4(0, 0, 0, 0);
+        if (ok)
+          for (int e = 0; e < EPC; ++e)
+            if (c + e < p.C) t.e[e] = Ag[off + e];
+        ra[q] = t.u;
       }
-      ra[q] = v;
     }
     // B (packed weights, always in range)
 #pragma unroll
@@ -154,7 +157,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
 #pragma unroll
     for (int q = 0; q < RA; ++q) {
       int r = rsub + 32 * q;
-      As[r * 8 + (chunk ^ ((r >> 1) & 7))] = ra[q];
+      uint4 v = ra[q];
+      if (p.vec_ok) {
+        v = mask_chunk<EPC>(v, a_c, p.C);
+        if (!((a_ok >> q) & 1u)) v = make_uint4(0, 0, 0, 0);
+      }
+      As[r * 8 + (chunk ^ ((r >> 1) & 7))] = v;
     }
 #pragma unroll
     for (int q = 0; q < RB; ++q) {

@@ -26,6 +26,24 @@ struct FastDiv {
   }
 };
 
+// Zero the elements of a 16-byte chunk whose channel index (c0 + e) is >= C.
+// Branch-free (selects only) so hipcc keeps loads in flight (no per-element vmcnt(0)).
+template <int EPC>
+__device__ __forceinline__ uint4 mask_chunk(uint4 v, int c0, int C) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if constexpr (EPC == 8) {  // two bf16 per dword
+      const int e = c0 + 2 * d;
+      uint32_t m = (e + 1 < C) ? 0xFFFFFFFFu : ((e < C) ? 0x0000FFFFu : 0u);
+      w[d] &= m;
+    } else {
+      w[d] = (c0 + d < C) ? w[d] : 0u;
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // ---------------------------------------------------------------- implicit GEMM ----
 // Out[row][n'] = sum_{tap, c} A[pix(row, tap)][c] * Wp[n'][tap][c]   (+ epilogue)
 // row enumerates an output sub-grid (n, j, i): output pixel (oy0 + osy*j, ox0 + osx*i);
@@ -112,6 +130,31 @@ struct EpiArgs {               // split-K finalize
   int dtype;
 };
 
+// ---------------------------------------------------------------- halo direct conv ----
+// Stride-1 (sub-)grid conv: output (sub-grid) pixel (j, i) reads A at (j + dy[t], i + dx[t]).
+struct HaloArgs {
+  const void* A;
+  int64_t a_sn, a_sh, a_sw;
+  int A_H, A_W, C;
+  int nks;                    // 64-byte channel steps = ceil(C / KS)
+  int ntaps;
+  int dymin, dxmin, HH, HW;   // halo = (TH + dy range) x (TW + dx range)
+  int pad_mode, vec_ok;        // vec_ok: 16-byte loads of whole chunks stay inside each pixel row
+  int N, JH, JW, tiles_h, tiles_w;
+  const void* Wp;             // [nks*ntaps][ntiles][rup(BN,128)][64 B], rows pre-swizzled
+  int ntiles, BN, Nout;
+  void* Y;
+  int64_t y_sn, y_sh, y_sw;
+  int oy0, ox0, osy, osx;
+  const float* bias;
+  const void* R;
+  int64_t r_sn, r_sh, r_sw;
+  float res_scale;
+  int act;
+  float slope;
+  int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
+};
+
 // launchers (return hipError_t as int); cfg selects the tile shape
 int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s);
 int igemm_cfg_bn(int cfg);
@@ -121,5 +164,9 @@ int wgrad_cfg_bm(int cfg);
 int wgrad_cfg_bn(int cfg);
 int launch_pack(const PackArgs& a, hipStream_t s);
 int launch_epilogue(const EpiArgs& a, hipStream_t s);
+int halo_cfg(int tw, int kspan, int bn);
+int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);
+int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
+size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
 
 }  // namespace tpg

@@ -73,30 +73,34 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs p) {
   const int dy = s_dy[tap], dx = s_dx[tap];
 
   uint4 ra[LA], rb[LB];
+  uint32_t okA = 0, okB = 0;
   auto load_tile = [&](int p0) {
+    okA = 0;
+    okB = 0;
 #pragma unroll
     for (int q = 0; q < LA; ++q) {
       int idx = tid + 256 * q;
       int row = idx / CPR_A, ch = idx % CPR_A;
       int pix = p0 + row;
       int c = a0 + ch * EPC;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (pix < pend && c < p.Ca) {
-        int n = p.div_phpw.div(pix);
-        int rem = pix - n * PHPW;
-        int py = p.div_pw.div(rem);
-        int px = rem - py * p.PW;
-        const E* src = Pg + (int64_t)n * p.p_sn + (int64_t)py * p.p_sh + (int64_t)px * p.p_sw + c;
-        if (p.vec_p && c + EPC <= p.Ca) {
-          v = *reinterpret_cast<const uint4*>(src);
-        } else {
-          union { uint4 u; E e[EPC]; } t;
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) t.e[e] = (c + e < p.Ca) ? src[e] : (E)0.f;
-          v = t.u;
-        }
+      const bool ok = pix < pend && c < p.Ca;
+      int pp = ok ? pix : pbeg;
+      int n = p.div_phpw.div(pp);
+      int rem = pp - n * PHPW;
+      int py = p.div_pw.div(rem);
+      int px = rem - py * p.PW;
+      const int64_t off = (int64_t)n * p.p_sn + (int64_t)py * p.p_sh + (int64_t)px * p.p_sw + c;
+      okA |= (ok ? 1u : 0u) << q;
+      if (p.vec_p) {
+        ra[q] = *reinterpret_cast<const uint4*>(Pg + (ok ? off : 0));  // masked at store time
+      } else {
+        union { uint4 u; E e[EPC]; } t;
+        t.u = make_uint4(0, 0, 0, 0);
+        if (ok)
+          for (int e = 0; e < EPC; ++e)
+            if (c + e < p.Ca) t.e[e] = Pg[off + e];
+        ra[q] = t.u;
       }
-      ra[q] = v;
     }
 #pragma unroll
     for (int q = 0; q < LB; ++q) {
@@ -104,27 +108,27 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs p) {
       int row = idx / CPR_B, ch = idx % CPR_B;
       int pix = p0 + row;
       int c = b0 + ch * EPC;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (pix < pend && c < p.Cb) {
-        int n = p.div_phpw.div(pix);
-        int rem = pix - n * PHPW;
-        int py = p.div_pw.div(rem);
-        int px = rem - py * p.PW;
-        int qy = py * p.qst_h + dy, qx = px * p.qst_w + dx;
-        if (p.pad_mode) { qy = refl(qy, p.QH); qx = refl(qx, p.QW); }
-        if ((unsigned)qy < (unsigned)p.QH && (unsigned)qx < (unsigned)p.QW) {
-          const E* src = Qg + (int64_t)n * p.q_sn + (int64_t)qy * p.q_sh + (int64_t)qx * p.q_sw + c;
-          if (p.vec_q && c + EPC <= p.Cb) {
-            v = *reinterpret_cast<const uint4*>(src);
-          } else {
-            union { uint4 u; E e[EPC]; } t;
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) t.e[e] = (c + e < p.Cb) ? src[e] : (E)0.f;
-            v = t.u;
-          }
-        }
+      bool ok = pix < pend && c < p.Cb;
+      int pp = ok ? pix : pbeg;
+      int n = p.div_phpw.div(pp);
+      int rem = pp - n * PHPW;
+      int py = p.div_pw.div(rem);
+      int px = rem - py * p.PW;
+      int qy = py * p.qst_h + dy, qx = px * p.qst_w + dx;
+      if (p.pad_mode) { qy = refl(qy, p.QH); qx = refl(qx, p.QW); }
+      ok = ok && (unsigned)qy < (unsigned)p.QH && (unsigned)qx < (unsigned)p.QW;
+      const int64_t off = (int64_t)n * p.q_sn + (int64_t)qy * p.q_sh + (int64_t)qx * p.q_sw + c;
+      okB |= (ok ? 1u : 0u) << q;
+      if (p.vec_q) {
+        rb[q] = *reinterpret_cast<const uint4*>(Qg + (ok ? off : 0));  // masked at store time
+      } else {
+        union { uint4 u; E e[EPC]; } t;
+        t.u = make_uint4(0, 0, 0, 0);
+        if (ok)
+          for (int e = 0; e < EPC; ++e)
+            if (c + e < p.Cb) t.e[e] = Qg[off + e];
+        rb[q] = t.u;
       }
-      rb[q] = v;
     }
   };
 
@@ -135,13 +139,23 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs p) {
     for (int q = 0; q < LA; ++q) {
       int idx = tid + 256 * q;
       int row = idx / CPR_A, ch = idx % CPR_A;
-      As[row * CPR_A + swz<BF, BM>(row, ch)] = ra[q];
+      uint4 v = ra[q];
+      if (p.vec_p) {
+        v = mask_chunk<EPC>(v, a0 + ch * EPC, p.Ca);
+        if (!((okA >> q) & 1u)) v = make_uint4(0, 0, 0, 0);
+      }
+      As[row * CPR_A + swz<BF, BM>(row, ch)] = v;
     }
 #pragma unroll
     for (int q = 0; q < LB; ++q) {
       int idx = tid + 256 * q;
       int row = idx / CPR_B, ch = idx % CPR_B;
-      Bs[row * CPR_B + swz<BF, BN>(row, ch)] = rb[q];
+      uint4 v = rb[q];
+      if (p.vec_q) {
+        v = mask_chunk<EPC>(v, b0 + ch * EPC, p.Cb);
+        if (!((okB >> q) & 1u)) v = make_uint4(0, 0, 0, 0);
+      }
+      Bs[row * CPR_B + swz<BF, BN>(row, ch)] = v;
     }
   };
 
