@@ -562,6 +562,34 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   a.w_sa = dw.stride[0]; a.w_sb = dw.stride[1]; a.w_sr = dw.stride[2]; a.w_ss = dw.stride[3];
   a.div_pw.init(a.PW);
   a.div_phpw.init(a.PH * a.PW);
+  // pipelined DMA kernel when both operands are 16-byte aligned channels-last rows
+  if (a.vec_p && a.vec_q) {
+    static const int cand[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    int bm = 0, bn = 0;
+    int64_t best = -1;
+    for (auto& c : cand) {
+      // padded MACs, small tiles charged 15% for their lower operand reuse
+      int64_t cost = (int64_t)rup(a.Ca, c[0]) * rup(a.Cb, c[1]) * ((c[0] == 64 || c[1] == 64) ? 115 : 100);
+      if (best < 0 || cost < best) { best = cost; bm = c[0]; bn = c[1]; }
+    }
+    const int kp = d->dtype == TPG_BF16 ? 64 : 32;
+    const int tiles = cdiv(a.Ca, bm) * cdiv(a.Cb, bn) * a.ntaps;
+    int ks = std::max(1, cdiv(2048, tiles));
+    ks = std::min(ks, std::max(1, a.npix / (kp * 8)));
+    a.pix_per_split = (int)rup(cdiv(a.npix, ks), kp);
+    a.ksplit = cdiv(a.npix, a.pix_per_split);
+    const int es = esize(d->dtype);
+    auto extent = [&](const tpg_tensor& t, int n, int h, int w, int c) -> int64_t {
+      return ((int64_t)(n - 1) * t.stride[0] + (int64_t)(h - 1) * t.stride[2] + (int64_t)(w - 1) * t.stride[3] + c) * es;
+    };
+    const int64_t pb = extent(P, d->n, a.PH == 1 && comp ? 1 : PH, a.PW == 1 && comp ? 1 : PW, a.Ca);
+    const int64_t qb = comp ? extent(Q, d->n, 1, 1, a.Cb) : extent(Q, d->n, QH, QW, cb);
+    if (pb < (1ll << 31) && qb < (1ll << 31)) {
+      a.p_bytes = (int)pb;
+      a.q_bytes = (int)qb;
+      return hip_check(launch_wgrad2(a, d->dtype, wgrad2_cfg(bm, bn), bm, bn, (hipStream_t)stream), "wgrad2");
+    }
+  }
   const int cfg = (a.Ca >= 128 && a.Cb >= 128) ? 1 : 0;
   const int bm = wgrad_cfg_bm(cfg), bn = wgrad_cfg_bn(cfg);
   const int tiles = cdiv(a.Ca, bm) * cdiv(a.Cb, bn) * a.ntaps;

@@ -12,17 +12,18 @@ namespace tpg {
 // Fast unsigned division by a runtime constant for n, d < 2^31 (round-up method):
 // s = ceil(log2 d), mul = ceil(2^(31+s) / d) < 2^32, q = umulhi(n, mul) >> (s - 1).
 struct FastDiv {
-  uint32_t d, mul, shift;
+  uint32_t d, mul, shift, dmask;  // dmask = ~0 for d == 1 (q = n), else 0: branch-free
   __host__ void init(uint32_t div) {
-    d = div;
-    if (div <= 1) { d = 1; mul = 0; shift = 0; return; }
+    d = div < 1 ? 1 : div;
+    if (d == 1) { mul = 0; shift = 0; dmask = 0xFFFFFFFFu; return; }
     uint32_t s = 0;
-    while ((1u << s) < div) ++s;
-    mul = (uint32_t)(((1ull << (31 + s)) + div - 1) / div);
+    while ((1u << s) < d) ++s;
+    mul = (uint32_t)(((1ull << (31 + s)) + d - 1) / d);
     shift = s - 1;
+    dmask = 0;
   }
   __device__ __forceinline__ uint32_t div(uint32_t n) const {
-    return d == 1 ? n : (__umulhi(n, mul) >> shift);
+    return (__umulhi(n, mul) + (n & dmask)) >> shift;
   }
 };
 
@@ -97,7 +98,9 @@ struct WgradArgs {
   int ksplit, pix_per_split;
   FastDiv div_pw, div_phpw;
   int8_t dy[TPG_MAX_TAPS], dx[TPG_MAX_TAPS], tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
+  int p_bytes, q_bytes;       // buffer extents for the DMA kernel (out-of-range reads -> 0)
 };
+typedef WgradArgs Wgrad2Args;
 
 // ---------------------------------------------------------------- weight packing ----
 // Wp[n'][unit*16 + e] = W[a][b][r][s] (fp32 master -> compute dtype, zero padded).
@@ -163,6 +166,8 @@ int launch_wgrad(const WgradArgs& a, int dtype, int cfg, hipStream_t s);
 int wgrad_cfg_bm(int cfg);
 int wgrad_cfg_bn(int cfg);
 int launch_pack(const PackArgs& a, hipStream_t s);
+int wgrad2_cfg(int bm, int bn);
+int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s);
 int launch_epilogue(const EpiArgs& a, hipStream_t s);
 int halo_cfg(int tw, int kspan, int bn);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);

@@ -1,0 +1,295 @@
+// Weight gradient, pipelined (gfx950): dW[a][b][r][s] += sum_p P[p][a] * Q[gather_t(p)][b].
+//
+// Same problem as tpg_wgrad.hip (P = the pixel-grid operand, Q = the gathered one; see
+// there for the Conv2d / ConvTranspose2d role mapping) restructured around the pipeline
+// rules that made the halo kernel fast:
+//   - 8 waves, block tile BM (a) x BN (b), K = pixels in tiles of KP (bf16: 64, f32: 32);
+//   - both operand tiles arrive by buffer LDS-DMA (buffer_load_dwordx4 ... lds) into a
+//     3-stage LDS ring, two k-tiles ahead; a pixel outside the image (or past the block's
+//     pixel range) gets an offset beyond the buffer's num_records, which the hardware
+//     returns as zero: padding costs no instruction;
+//   - the LDS image is lane-linear (DMA), so the bank swizzle is applied to the SOURCE
+//     address: LDS chunk c of row r holds logical chunk c ^ swz(r), and readers XOR back;
+//   - one counted s_waitcnt vmcnt(pieces per k-tile) + lgkmcnt(0) + s_barrier per k-tile.
+// Channel tails: a 16-byte chunk that straddles Ca / Cb reads a few channels past the
+// tensor's real channels (inside the padded pixel row); they only feed dW rows / columns
+// that are never written.
+#include "tpg_internal.h"
+#include <type_traits>
+
+namespace tpg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ int w2_refl(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+// ds_read_b64_tr_b16 through inline asm (see compute())
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  s16x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+// chunk swizzle of an LDS row of RB bytes (see tpg_wgrad.hip for the tr-read analysis)
+template <bool BF, int RB>
+__device__ __forceinline__ int w2_swz(int row) {
+  if constexpr (BF) {
+    if constexpr (RB == 128) return ((((row >> 1) & 1) | (((row >> 3) & 1) << 1))) << 1;
+    else return (((row & 3) | (((row >> 3) & 1) << 2))) << 1;
+  } else {
+    return (row & 1) << 2;
+  }
+}
+
+template <bool BF, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
+  using E = typename std::conditional<BF, __bf16, float>::type;
+  constexpr int ES = sizeof(E);
+  constexpr int EPC = 16 / ES;
+  constexpr int KP = BF ? 64 : 32;            // pixels per k-tile
+  constexpr int RBA = BM * ES, RBB = BN * ES;  // LDS row bytes
+  constexpr int CPRA = RBA / 16, CPRB = RBB / 16;
+  constexpr int BYTES_A = KP * RBA, BYTES_B = KP * RBB;
+  constexpr int GA = BYTES_A / 8192, GB = BYTES_B / 8192;  // 1 KiB DMA pieces per wave
+  constexpr int STAGE = BYTES_A + BYTES_B;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MREP = WTM / 16, NREP = WTN / 16;
+  static_assert(GA * 8192 == BYTES_A && GB * 8192 == BYTES_B && GA >= 1 && GB >= 1, "tile bytes");
+  static_assert(WM * WN == 8 && MREP * 16 * WM == BM && NREP * 16 * WN == BN, "waves");
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [3][STAGE]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nta = (p.Ca + BM - 1) / BM;
+  const int ta = blockIdx.x % nta, tb = blockIdx.x / nta;
+  const int a0 = ta * BM, b0 = tb * BN;
+  const int tap = blockIdx.y;
+  const int pbeg = blockIdx.z * p.pix_per_split;
+  const int pend = min(p.npix, pbeg + p.pix_per_split);
+  const int nkt = (pend - pbeg + KP - 1) / KP;
+  const int dy = p.dy[tap], dx = p.dx[tap];
+  const int PHPW = p.PH * p.PW;
+  // kernel arguments used in the DMA address math, hoisted once
+  const FastDiv dv_phpw = p.div_phpw, dv_pw = p.div_pw;
+  const int PW = p.PW, QH = p.QH, QW = p.QW, qsh = p.qst_h, qsw = p.qst_w, pad_mode = p.pad_mode;
+  const int Ca = p.Ca, Cb = p.Cb;
+  const int64_t psn = p.p_sn, psh = p.p_sh, psw = p.p_sw, qsn = p.q_sn, qsh_ = p.q_sh, qsw_ = p.q_sw;
+
+  const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.P), 0, p.p_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Q), 0, p.q_bytes, 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+
+  // DMA of k-tile kt into ring slot `slot`
+  auto issue = [&](int kt, int slot) {
+    char* st = lds + slot * STAGE;
+    const int p0 = pbeg + kt * KP;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int o = (wave * GA + j) * 1024 + lane * 16;  // byte offset in the A image
+      const int row = o / RBA, pc = (o % RBA) / 16;
+      const int lc = pc ^ w2_swz<BF, RBA>(row);
+      const int pix = p0 + row;
+      const int c = a0 + lc * EPC;
+      unsigned off = OOB;
+      {
+        const int n = dv_phpw.div(pix), rem = pix - n * PHPW;
+        const int py = dv_pw.div(rem), px = rem - py * PW;
+        const unsigned o2 = (unsigned)((n * psn + py * psh + px * psw + c) * ES);
+        off = (pix < pend && c < Ca) ? o2 : OOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(st + (wave * GA + j) * 1024),
+                                               16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int o = (wave * GB + j) * 1024 + lane * 16;
+      const int row = o / RBB, pc = (o % RBB) / 16;
+      const int lc = pc ^ w2_swz<BF, RBB>(row);
+      const int pix = p0 + row;
+      const int c = b0 + lc * EPC;
+      unsigned off = OOB;
+      {
+        const int n = dv_phpw.div(pix), rem = pix - n * PHPW;
+        const int py = dv_pw.div(rem), px = rem - py * PW;
+        int qy = py * qsh + dy, qx = px * qsw + dx;
+        if (pad_mode) { qy = w2_refl(qy, QH); qx = w2_refl(qx, QW); }
+        const bool ok = pix < pend && c < Cb && (unsigned)qy < (unsigned)QH && (unsigned)qx < (unsigned)QW;
+        const unsigned o2 = (unsigned)((n * qsn + qy * qsh_ + qx * qsw_ + c) * ES);
+        off = ok ? o2 : OOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rQ, (__attribute__((address_space(3))) void*)(st + BYTES_A + (wave * GB + j) * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, l16 = lane & 15;
+  f32x4 acc[MREP][NREP];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m)
+#pragma unroll
+    for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int slot) {
+    const char* A = lds + slot * STAGE;
+    const char* B = A + BYTES_A;
+    if constexpr (BF) {
+      const int q = l16 >> 2, p4 = l16 & 3;
+#pragma unroll
+      for (int ks = 0; ks < KP / 32; ++ks) {
+        bf16x8 af[MREP], bfr[NREP];
+#pragma unroll
+        for (int m = 0; m < MREP; ++m) {
+          const int col = wm * WTM + m * 16 + 4 * p4;
+          s16x4 h[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int row = ks * 32 + 8 * g + 4 * hh + q;
+            const char* ad = A + row * RBA + (((col >> 3) ^ w2_swz<BF, RBA>(row)) << 4) + (col & 7) * 2;
+            h[hh] = tr_read(ad);
+          }
+          af[m] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[0], h[1], 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int n = 0; n < NREP; ++n) {
+          const int col = wn * WTN + n * 16 + 4 * p4;
+          s16x4 h[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int row = ks * 32 + 8 * g + 4 * hh + q;
+            const char* ad = B + row * RBB + (((col >> 3) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 7) * 2;
+            h[hh] = tr_read(ad);
+          }
+          bfr[n] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[0], h[1], 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        // the tr reads are inline asm (invisible to hipcc's LDS-DMA alias tracking, which
+        // would otherwise put a vmcnt(0) in front of them): wait for them by hand and keep
+        // the MFMAs below the wait (§5.4 rule 18)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < MREP; ++m)
+#pragma unroll
+          for (int n = 0; n < NREP; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KP / 4; ++kk) {
+        const int row = 4 * kk + g;
+        float av[MREP], bv[NREP];
+#pragma unroll
+        for (int m = 0; m < MREP; ++m) {
+          const int col = wm * WTM + m * 16 + l16;
+          av[m] = *reinterpret_cast<const float*>(A + row * RBA + (((col >> 2) ^ w2_swz<BF, RBA>(row)) << 4) + (col & 3) * 4);
+        }
+#pragma unroll
+        for (int n = 0; n < NREP; ++n) {
+          const int col = wn * WTN + n * 16 + l16;
+          bv[n] = *reinterpret_cast<const float*>(B + row * RBB + (((col >> 2) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 3) * 4);
+        }
+#pragma unroll
+        for (int m = 0; m < MREP; ++m)
+#pragma unroll
+          for (int n = 0; n < NREP; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+      }
+    }
+  };
+
+#define W2_WAIT_BARRIER()                                                                          \
+  do {                                                                                             \
+    if constexpr (GA + GB == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else if constexpr (GA + GB == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else if constexpr (GA + GB == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else if constexpr (GA + GB == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
+  } while (0)
+
+  if (nkt > 0) {
+    issue(0, 0);
+    issue(min(1, nkt - 1), 1);
+    W2_WAIT_BARRIER();  // retires k-tile 0
+    int slot = 0;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int slot2 = slot == 0 ? 2 : slot - 1;
+      issue(min(kt + 2, nkt - 1), slot2);  // unconditional (clamped): static vmcnt
+      compute(slot);
+      W2_WAIT_BARRIER();                   // retires k-tile kt+1, kt+2 stays in flight
+      slot = slot == 2 ? 0 : slot + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#undef W2_WAIT_BARRIER
+
+  // ---- epilogue: fp32 atomics into dW (C/D layout: col = lane&15 -> b, row = 4g+reg -> a)
+  const int r_tap = p.tr[tap], s_tap = p.ts[tap];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int a = a0 + wm * WTM + m * 16 + 4 * g + reg;
+      if (a >= p.Ca) continue;
+#pragma unroll
+      for (int n = 0; n < NREP; ++n) {
+        const int bq = b0 + wn * WTN + n * 16 + l16;
+        if (bq >= p.Cb) continue;
+        int r = r_tap, s = s_tap, b = bq;
+        if (p.bcomp) {
+          const int rs = bq / p.comp_cb;
+          b = bq - rs * p.comp_cb;
+          r = rs / p.comp_kw;
+          s = rs - r * p.comp_kw;
+        }
+        atomicAdd(p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss, acc[m][n][reg]);
+      }
+    }
+}
+
+// {id, BM, BN, WM, WN}
+#define TPG_WGRAD2_CFGS(X) \
+  X(0, 64, 64, 4, 2)       \
+  X(1, 64, 128, 2, 4)      \
+  X(2, 128, 64, 4, 2)      \
+  X(3, 128, 128, 2, 4)     \
+  X(4, 256, 128, 4, 2)
+
+int wgrad2_cfg(int bm, int bn) {
+#define X(id, BM_, BN_, WM_, WN_) if (bm == BM_ && bn == BN_) return id;
+  TPG_WGRAD2_CFGS(X)
+#undef X
+  return -1;
+}
+
+int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s) {
+  dim3 grid(((a.Ca + bm - 1) / bm) * ((a.Cb + bn - 1) / bn), a.ntaps, a.ksplit);
+#define X(id, BM_, BN_, WM_, WN_)                                                                       \
+  if (cfg == (id)) {                                                                                    \
+    if (dtype == 1) {                                                                                   \
+      auto k = wgrad2_kernel<true, BM_, BN_, WM_, WN_>;                                                 \
+      const size_t lds = 3 * 64 * (BM_ + BN_) * 2;                                                      \
+      static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                    (int)lds), true);                                   \
+      (void)once;                                                                                       \
+      hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                \
+    } else {                                                                                            \
+      auto k = wgrad2_kernel<false, BM_, BN_, WM_, WN_>;                                                \
+      const size_t lds = 3 * 32 * (BM_ + BN_) * 4;                                                      \
+      static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                    (int)lds), true);                                   \
+      (void)once;                                                                                       \
+      hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                \
+    }                                                                                                   \
+    return (int)hipGetLastError();                                                                      \
+  }
+  TPG_WGRAD2_CFGS(X)
+#undef X
+  return -1;
+}
+
+}  // namespace tpg
