@@ -207,7 +207,7 @@ static int32_t check_desc(const tpg_conv_desc* d) {
 static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   IgemmArgs& a = P.a;
   if (!unit_stride || a.ntaps < 1 || a.C < 1) return;
-  if (a.JW < 16 || (int64_t)a.JH * a.JW < 1024) return;
+  if (a.JW < 16 || (int64_t)a.JH * a.JW < 256) return;
   int dymin = 127, dymax = -128, dxmin = 127, dxmax = -128;
   for (int t = 0; t < a.ntaps; ++t) {
     dymin = std::min<int>(dymin, a.dy[t]); dymax = std::max<int>(dymax, a.dy[t]);

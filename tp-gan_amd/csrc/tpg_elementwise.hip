@@ -96,6 +96,49 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(int N, int C, int H, int W
   }
 }
 
+// Vector form for channels-last tensors with pixel-dense, 16-byte aligned rows: a thread
+// owns one 16-byte channel chunk and walks pixels, so its dbias partials stay in registers;
+// block partials are combined in LDS, then one global atomic per channel per block.
+template <typename E>
+__global__ __launch_bounds__(256) void act_bwd_vec_kernel(int64_t npix, int C, int act, float slope, const E* gy,
+                                                          int64_t gps, const E* y, int64_t yps, E* g, int64_t gps_out,
+                                                          float* dbias) {
+  constexpr int EPC = 16 / sizeof(E);
+  __shared__ float sb[1024];
+  const int nch = (C + EPC - 1) / EPC;
+  const int ppi = 256 / nch;                      // pixels per block iteration
+  const int ch = threadIdx.x % nch, pl = threadIdx.x / nch;
+  const bool active = pl < ppi;
+  for (int i = threadIdx.x; i < nch * EPC; i += 256) sb[i] = 0.f;
+  __syncthreads();
+  float part[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) part[e] = 0.f;
+  const int c0 = ch * EPC;
+  if (active) {
+    for (int64_t pix = (int64_t)blockIdx.x * ppi + pl; pix < npix; pix += (int64_t)gridDim.x * ppi) {
+      union { uint4 u; E e[EPC]; } vg, vy, vo;
+      vg.u = *reinterpret_cast<const uint4*>(gy + pix * gps + c0);
+      if (act != TPG_ACT_NONE) vy.u = *reinterpret_cast<const uint4*>(y + pix * yps + c0);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float v = (float)vg.e[e];
+        if (act != TPG_ACT_NONE && !((float)vy.e[e] > 0.f)) v = (act == TPG_ACT_LEAKY) ? v * slope : 0.f;
+        if (c0 + e >= C) v = 0.f;
+        vo.e[e] = (E)v;
+        part[e] += v;
+      }
+      *reinterpret_cast<uint4*>(g + pix * gps_out + c0) = vo.u;
+    }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e)
+      if (c0 + e < C) atomicAdd(&sb[c0 + e], part[e]);
+  }
+  __syncthreads();
+  if (dbias)
+    for (int i = threadIdx.x; i < C; i += 256) atomicAdd(dbias + i, sb[i]);
+}
+
 // ------------------------------------------------------------ strided 4-D copy --
 __global__ __launch_bounds__(256) void copy4d_kernel(int N, int C, int H, int W, tpg_tensor in, tpg_tensor out) {
   const int64_t total = (int64_t)N * C * H * W;
@@ -258,8 +301,34 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
 
 using namespace tpg;
 
+static bool pix_dense_vec(const tpg_tensor& t, int h, int w, int dtype, int c) {
+  const int es = dtype == TPG_BF16 ? 2 : 4, epc = 16 / es;
+  if (t.dtype != dtype || t.stride[1] != 1) return false;
+  const int64_t ps = t.stride[3];
+  if (ps % epc || ps < (c + epc - 1) / epc * epc) return false;
+  if (t.stride[2] != ps * w || t.stride[0] != ps * w * h) return false;
+  return ((uintptr_t)t.data % 16) == 0;
+}
+
 extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
                                      tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, hipStream_t s) {
+  const int dt = g.dtype;
+  const int epc = dt == TPG_BF16 ? 8 : 4;
+  if (c <= 1024 && (c + epc - 1) / epc <= 256 && pix_dense_vec(gy, h, w, dt, c) && pix_dense_vec(g, h, w, dt, c) &&
+      (act == TPG_ACT_NONE || pix_dense_vec(y, h, w, dt, c))) {
+    const int64_t npix = (int64_t)n * h * w;
+    const int ppi = 256 / ((c + epc - 1) / epc);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((npix + ppi - 1) / ppi, 2048));
+    if (dt == TPG_BF16)
+      hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, npix, c, act, slope,
+                         (const __bf16*)gy.data, gy.stride[3], (const __bf16*)y.data, y.stride[3], (__bf16*)g.data,
+                         g.stride[3], dbias);
+    else
+      hipLaunchKernelGGL(act_bwd_vec_kernel<float>, dim3(blocks), dim3(256), 0, s, npix, c, act, slope,
+                         (const float*)gy.data, gy.stride[3], (const float*)y.data, y.stride[3], (float*)g.data,
+                         g.stride[3], dbias);
+    return (int)hipGetLastError();
+  }
   int64_t npix = (int64_t)n * h * w;
   int gx = (int)std::min<int64_t>((npix + 63) / 64, 2048);
   if (gx < 1) gx = 1;

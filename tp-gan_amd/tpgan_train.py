@@ -68,6 +68,29 @@ class FlatParams:
                             weight_decay, self.step, grad_scale)
 
 
+class GradSync:
+    """Data-parallel exchange of one FlatParams: parameters broadcast from
+    rank 0 once, gradients summed with one all-reduce per network per step (RCCL over
+    xGMI with backend "nccl"; gloo on CPU for tests).  The 1/world average is folded into
+    the optimizer's grad_scale, so no extra pass over the gradients is made."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+    def broadcast(self, flat):
+        if self.world > 1:
+            dist.broadcast(flat.data, 0, group=self.group)
+
+    def allreduce(self, flat):
+        if self.world > 1:
+            dist.all_reduce(flat.grad, group=self.group)
+
+    @property
+    def grad_scale(self):
+        return 1.0 / self.world
+
+
 def total_variation(x):
     return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
 
@@ -92,16 +115,14 @@ class TPGANTrainer:
         self.gp = gradient_penalty
         if gradient_penalty:
             raise NotImplementedError("WGAN-GP needs double backward through the HIP convs (next round)")
-        self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.sync = GradSync(process_group)
+        self.world = self.sync.world
         self.identity_fn = identity_fn
-        if self.world > 1:
-            dist.broadcast(self.fG.data, 0, group=process_group)
-            dist.broadcast(self.fD.data, 0, group=process_group)
+        self.sync.broadcast(self.fG)
+        self.sync.broadcast(self.fD)
 
     def _allreduce(self, flat):
-        if self.world > 1:
-            dist.all_reduce(flat.grad, group=self.pg)
+        self.sync.allreduce(flat)
 
     def step(self, b):
         w = self.w
@@ -119,7 +140,7 @@ class TPGANTrainer:
             loss_D = d_fake.mean() - d_real.mean()
             loss_D.backward()
             self._allreduce(self.fD)
-            self.fD.adam(self.lr, self.betas, grad_scale=1.0 / self.world)
+            self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
             # ---- G-step through the frozen, updated D
             set_requires_grad(D.parameters(), False)
             d_gen = D(fake).float()
@@ -142,7 +163,7 @@ class TPGANTrainer:
             loss_G = loss_G + w["weight_identity_preserving"] * self.identity_fn(f32, front)
         loss_G.backward()
         self._allreduce(self.fG)
-        self.fG.adam(self.lr, self.betas, grad_scale=1.0 / self.world)
+        self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
         return {"loss_D": loss_D.detach(), "loss_G": loss_G.detach()}
 
 
