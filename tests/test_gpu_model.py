@@ -15,8 +15,7 @@ G_OUT = ["I128_fake", "encoder_predict", "fused_local_fake", "le_fake", "re_fake
 INS = ["I128", "left_eye", "right_eye", "nose", "mouth", "z"]
 
 
-@pytest.fixture(scope="module")
-def e2e(gpu):
+def _e2e(gpu, flat):
     import D_and_G_model as DG
     E = golden("e2e_golden.npz")
     G = DG.Generator(64, 347, use_batchnorm=False)
@@ -24,6 +23,10 @@ def e2e(gpu):
     load_det(G, "G/", torch.float32)
     load_det(D, "D/", torch.float32)
     G, D = G.to(gpu), D.to(gpu)
+    if flat:  # the train step's layout: params/grads are views of flat buffers, fused dW/db accumulation
+        import tpgan_train
+        G._flat = tpgan_train.FlatParams(G, gpu)
+        D._flat = tpgan_train.FlatParams(D, gpu)
     ins = {k: torch.from_numpy(E["in:" + k]).float().to(gpu).requires_grad_(True) for k in INS}
     outs = G(ins["I128"], ins["left_eye"], ins["right_eye"], ins["nose"], ins["mouth"], ins["z"], False)
     loss = 0
@@ -39,6 +42,16 @@ def e2e(gpu):
     loss.backward()
     torch.cuda.synchronize()
     return E, G, D, ins, outs, d_fake
+
+
+@pytest.fixture(scope="module")
+def e2e(gpu):
+    return _e2e(gpu, False)
+
+
+@pytest.fixture(scope="module")
+def e2e_flat(gpu):
+    return _e2e(gpu, True)
 
 
 def test_generator_outputs(e2e):
@@ -93,3 +106,20 @@ def test_discriminator_real(e2e, gpu):
     with torch.no_grad():
         d = D(ins["I128"].detach())
     assert rel(d.cpu(), E["out:d_real"]) < 1e-3
+
+
+def test_fused_grad_accumulation(e2e_flat):
+    """Flat-buffer models (FlatParams: HIP dW / db added in place into the flat gradient)
+    reproduce the reference gradients, and a second backward accumulates (+=)."""
+    E, G, D, ins, outs, d_fake = e2e_flat
+    _check_gsum(E, "G", G)
+    _check_gsum(E, "D", D)
+    assert all(p.grad.data_ptr() >= G._flat.grad.data_ptr() for p in G.parameters())
+    g1 = D._flat.grad.clone()
+    D._flat.grad.zero_()
+    D(ins["I128"].detach()).sum().backward()
+    first = D._flat.grad.clone()
+    D(ins["I128"].detach()).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(D._flat.grad.cpu(), 2 * first.cpu()) < 1e-6
+    assert g1.abs().sum() > 0

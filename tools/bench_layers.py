@@ -31,6 +31,12 @@ SHAPES = {
     "enhance_16": (32, 768, 16, 16, 768, 3, 1, 1, False, 0, ACT_LEAKY, True),
     "up_128": (32, 208, 64, 64, 64, 3, 2, 1, True, 1, ACT_RELU, False),
     "enh_8": (32, 576, 8, 8, 576, 2, 1, 0, False, 0, ACT_LEAKY, True),
+    "conv4_res": (32, 512, 8, 8, 512, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "local_5": (32, 512, 5, 5, 512, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "local_10": (32, 256, 10, 10, 256, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "local_20": (32, 128, 20, 20, 128, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "local_40": (32, 64, 40, 40, 64, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "conv4_s2": (32, 256, 16, 16, 512, 3, 2, 1, False, 0, ACT_LEAKY, False),
 }
 
 
@@ -43,7 +49,7 @@ def flops(s):
     return 2 * N * OH * OW * Cout * Cin * k * k
 
 
-def run(name, s, iters):
+def run(name, s, iters, passes):
     lib = load()
     dev = torch.device("cuda", 0)
     N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
@@ -74,6 +80,8 @@ def run(name, s, iters):
     f = flops(s)
     out = []
     for kind, fn in calls.items():
+        if kind not in passes:
+            continue
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -93,11 +101,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
     for name, s in SHAPES.items():
         if a.only and name not in a.only.split(","):
             continue
-        run(name, s, a.iters)
+        run(name, s, a.iters, a.passes.split(","))
 
 
 if __name__ == "__main__":

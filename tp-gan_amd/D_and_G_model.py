@@ -166,6 +166,11 @@ class GlobalPathway(nn.Module):
         self.decoded_img128 = conv(n_FM_decoder_conv[1], 3, 3, 1, 1, None, activation=None)
 
     def forward(self, I128, local_fake_image, local_feature, z):
+        return self.decode_128(self.encode(I128, z), local_fake_image, local_feature)
+
+    def encode(self, I128, z):
+        """Everything that does not depend on the local pathways (:283-320): the encoder,
+        fc1/fc2, the decoder up to upsample_128 and add_conv_and_deconv_128."""
         cat = tpgan_ops.cat
         conv0 = self.conv0(I128)
         conv1 = self.conv1(conv0)
@@ -195,6 +200,12 @@ class GlobalPathway(nn.Module):
         enhance_features_64 = self.enhance_features_64(cat([upsample_64, add_conv_and_deconv_64]))
         upsample_128 = self.upsample_128(enhance_features_64)
         add_conv_and_deconv_128 = self.add_conv_and_deconv_128(cat([deconv_128, conv0, I128]))
+        return upsample_128, add_conv_and_deconv_128, fc2
+
+    def decode_128(self, enc, local_fake_image, local_feature):
+        """The 128-px fusion with the local features (:321-329)."""
+        cat = tpgan_ops.cat
+        upsample_128, add_conv_and_deconv_128, fc2 = enc
         enhance_features_128 = self.enhance_features_128(
             cat([upsample_128, add_conv_and_deconv_128, local_feature, local_fake_image]))
         conv5 = self.conv5(enhance_features_128)
@@ -232,16 +243,37 @@ class Generator(nn.Module):
         self.feature_predict = FeaturePredict(num_classes)
 
     def forward(self, I128, left_eye, right_eye, nose, mouth, z, use_dropout):
-        left_eye_fake_image, left_eye_fake_feature = self.local_pathway_left_eye(left_eye)
-        right_eye_fake_image, right_eye_fake_feature = self.local_pathway_right_eye(right_eye)
-        nose_fake_image, nose_fake_feature = self.local_pathway_nose(nose)
-        mouth_fake_image, mouth_fake_feature = self.local_pathway_mouth(mouth)
+        paths = (self.local_pathway_left_eye, self.local_pathway_right_eye, self.local_pathway_nose,
+                 self.local_pathway_mouth)
+        patches = (left_eye, right_eye, nose, mouth)
+        if tpgan_ops.MULTISTREAM and I128.is_cuda:
+            # The four local pathways (small maps: kernels that fill few CUs) run on their
+            # own HIP streams, concurrently with the global pathway's local-independent part
+            # on the current stream; autograd replays each op's backward on its forward
+            # stream, so the backward overlaps the same way.
+            main = torch.cuda.current_stream()
+            side = tpgan_ops.side_streams(I128.device, 4)
+            outs = []
+            for st, path, x in zip(side, paths, patches):
+                st.wait_stream(main)
+                with torch.cuda.stream(st):
+                    outs.append(path(x))
+            enc = self.global_pathway.encode(I128, z)
+            for st, (img, feat) in zip(side, outs):
+                main.wait_stream(st)
+                img.record_stream(main)
+                feat.record_stream(main)
+        else:
+            outs = [path(x) for path, x in zip(paths, patches)]
+            enc = self.global_pathway.encode(I128, z)
+        ((left_eye_fake_image, left_eye_fake_feature), (right_eye_fake_image, right_eye_fake_feature),
+         (nose_fake_image, nose_fake_feature), (mouth_fake_image, mouth_fake_feature)) = outs
         fused_local_feature = self.local_fuser(left_eye_fake_feature, right_eye_fake_feature, nose_fake_feature,
                                                mouth_fake_feature)
         fused_local_fake_image = self.local_fuser(left_eye_fake_image, right_eye_fake_image, nose_fake_image,
                                                   mouth_fake_image)
         fused_local_origin_4_part = self.local_fuser(left_eye, right_eye, nose, mouth)
-        I128_fake, encoder_feature = self.global_pathway(I128, fused_local_fake_image, fused_local_feature, z)
+        I128_fake, encoder_feature = self.global_pathway.decode_128(enc, fused_local_fake_image, fused_local_feature)
         encoder_predict = self.feature_predict(encoder_feature, use_dropout)
         return (I128_fake, encoder_predict, fused_local_fake_image, left_eye_fake_image, right_eye_fake_image,
                 nose_fake_image, mouth_fake_image, fused_local_origin_4_part)

@@ -203,20 +203,42 @@ static int32_t check_desc(const tpg_conv_desc* d) {
   return 0;
 }
 
-// Route a unit-stride (sub-)grid problem to the halo kernel when it is big enough.
+// Route a unit-stride (sub-)grid problem to the halo kernel.  Tile choice: a TH x TW tile
+// of one image (large maps) or IMG whole images per 256-row block (small maps), minimising
+// computed rows x taps plus staged halo pixels; then a split over k-steps when the grid
+// has too few blocks to fill the chip (fp32 partial slices, summed by the epilogue).
 static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   IgemmArgs& a = P.a;
   if (!unit_stride || a.ntaps < 1 || a.C < 1) return;
-  if (a.JW < 16 || (int64_t)a.JH * a.JW < 256) return;
   int dymin = 127, dymax = -128, dxmin = 127, dxmax = -128;
   for (int t = 0; t < a.ntaps; ++t) {
     dymin = std::min<int>(dymin, a.dy[t]); dymax = std::max<int>(dymax, a.dy[t]);
     dxmin = std::min<int>(dxmin, a.dx[t]); dxmax = std::max<int>(dxmax, a.dx[t]);
   }
-  if (dymax - dymin > 6 || dxmax - dxmin > 6) return;
-  // tile width: the one wasting fewer columns (ties -> 32, smaller halo overhead)
-  const int w32 = cdiv(a.JW, 32) * 32, w16 = cdiv(a.JW, 16) * 16;
-  const int tw = (w32 <= w16) ? 32 : 16, th = 256 / tw;
+  const int sy = dymax - dymin + 1, sx = dxmax - dxmin + 1;
+  if (sy > 7 || sx > 7) return;
+  const int JH = a.JH, JW = a.JW;
+  const int HCAP = 5 * 128;
+  int bth = 0, btw = 0, bimg = 0;
+  int64_t bcost = -1;
+  auto consider = [&](int th, int tw, int img) {
+    if (th < 1 || tw < 1 || img < 1 || th * tw * img > 256) return;
+    const int hpi = (th + sy - 1) * (tw + sx - 1);
+    if ((int64_t)img * hpi > HCAP) return;
+    const int64_t nsub = (int64_t)N * cdiv(JH, th) * cdiv(JW, tw);
+    const int64_t blocks = (nsub + img - 1) / img;
+    const int64_t cost = blocks * (256 * (int64_t)a.ntaps + (int64_t)img * hpi);
+    if (bcost < 0 || cost < bcost) { bcost = cost; bth = th; btw = tw; bimg = img; }
+  };
+  if (JH * JW <= 256)
+    for (int img = std::min(256 / (JH * JW), N); img >= 1; --img) consider(JH, JW, img);
+  for (int tw : {JW, 64, 48, 40, 32, 24, 16, 8}) {
+    if (tw > JW || tw > 256) continue;
+    const int thmax = std::min(JH, 256 / tw);
+    if (thmax < 1) continue;
+    consider(cdiv(JH, cdiv(JH, thmax)), tw, 1);
+  }
+  if (bcost < 0) return;
   int bn;
   if (a.Nout <= 32) bn = 32;
   else if (a.Nout <= 64) bn = 64;
@@ -224,7 +246,9 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   else if (a.Nout <= 128) bn = 128;
   else if (a.Nout <= 224) bn = a.Nout > 192 ? 224 : 128;
   else bn = (cdiv(a.Nout, 224) * 224 < cdiv(a.Nout, 128) * 128) ? 224 : 128;
-  const int cfg = halo_cfg(tw, std::max(dymax - dymin, dxmax - dxmin) + 1, bn);
+  const int hcap = (int)rup((int64_t)bimg * (bth + sy - 1) * (btw + sx - 1), 8);
+  const int hl = std::max(3, cdiv(hcap * 4, 512));
+  const int cfg = halo_cfg(hl, bn);
   if (cfg < 0) return;
   HaloArgs& h = P.h;
   memset(&h, 0, sizeof(h));
@@ -233,19 +257,30 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   h.nks = cdiv(a.C, ks_elems);
   h.ntaps = a.ntaps;
   h.dymin = dymin; h.dxmin = dxmin;
-  h.HH = th + dymax - dymin; h.HW = tw + dxmax - dxmin;
+  h.TH = bth; h.TW = btw; h.IMG = bimg; h.SH = 1; h.SW = 1;
+  h.HH = bth + sy - 1; h.HW = btw + sx - 1;
+  h.hcap = hcap;
   for (int t = 0; t < a.ntaps; ++t) h.toff[t] = (a.dy[t] - dymin) * h.HW + (a.dx[t] - dxmin);
   h.pad_mode = a.pad_mode;
-  h.N = N; h.JH = a.JH; h.JW = a.JW;
-  h.tiles_h = cdiv(a.JH, th); h.tiles_w = cdiv(a.JW, tw);
+  h.N = N; h.JH = JH; h.JW = JW;
+  h.tiles_h = cdiv(JH, bth); h.tiles_w = cdiv(JW, btw);
   h.BN = bn; h.ntiles = cdiv(a.Nout, bn); h.Nout = a.Nout;
   h.oy0 = a.oy0; h.ox0 = a.ox0; h.osy = a.osy; h.osx = a.osx;
+  // split over k-steps until the grid covers the chip (each split >= 4 pipeline steps)
+  const int64_t base = (((int64_t)N * h.tiles_h * h.tiles_w + bimg - 1) / bimg) * h.ntiles;
+  int ks = 1;
+  if (base < 256) {
+    const int kps_min = cdiv(4, a.ntaps);
+    ks = (int)std::min<int64_t>(cdiv(256, (int)base), std::max(1, h.nks / kps_min));
+  }
+  h.kps = cdiv(h.nks, std::max(ks, 1));
+  h.ksplit = cdiv(h.nks, h.kps);
   P.halo = true;
   P.hcfg = cfg;
   P.g_wp = P.wp_bytes;
   P.g_sk = P.sk_bytes;
   P.wp_bytes = (size_t)rup((int64_t)halo_wp_bytes(h.nks, h.ntaps, bn, h.ntiles), 256);
-  P.sk_bytes = 0;
+  P.sk_bytes = h.ksplit > 1 ? (size_t)rup((int64_t)h.ksplit * a.M * a.Nout * 4, 256) : 0;
 }
 
 // ---- forward plans
@@ -397,13 +432,18 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
   size_t need = probs_ws(v);
   if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
   const bool vA = vec_ok(A, dtype);
-  if (!vA)  // the halo kernel only takes 16-byte aligned channels-last rows
-    for (Prob& P : v)
-      if (P.halo) {
-        P.halo = false;
-        P.wp_bytes = P.g_wp;
-        P.sk_bytes = P.g_sk;
-      }
+  for (Prob& P : v) {
+    if (!P.halo) continue;
+    // the halo kernel takes 16-byte aligned channels-last rows and keeps 32-bit element
+    // offsets into A
+    const int64_t ext = (int64_t)(P.h.N - 1) * std::abs(A.stride[0]) + (int64_t)(P.h.A_H - 1) * std::abs(A.stride[2]) +
+                        (int64_t)(P.h.A_W - 1) * std::abs(A.stride[3]) + P.h.C + 64;
+    if (!vA || ext >= (1ll << 31)) {
+      P.halo = false;
+      P.wp_bytes = P.g_wp;
+      P.sk_bytes = P.g_sk;
+    }
+  }
   size_t off = 0;
   std::vector<char*> wps;
   for (Prob& P : v) { wps.push_back(ws + off); off += std::max(P.wp_bytes, P.g_wp); }
@@ -428,8 +468,22 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
       h.bias = bias;
       h.R = R.data; h.r_sn = R.stride[0]; h.r_sh = R.stride[2]; h.r_sw = R.stride[3];
       h.res_scale = res_scale; h.act = act; h.slope = slope;
+      h.ws = h.ksplit > 1 ? reinterpret_cast<float*>(sk) : nullptr;
       int e = launch_halo(h, dtype, P.hcfg, s);
       if (e) return hip_check(e, "halo conv");
+      if (h.ksplit > 1) {
+        EpiArgs ep;
+        memset(&ep, 0, sizeof(ep));
+        ep.ws = h.ws; ep.nslices = h.ksplit; ep.slice = (int64_t)a.M * a.Nout;
+        ep.M = a.M; ep.Nout = a.Nout; ep.JH = a.JH; ep.JW = a.JW;
+        ep.Y = Y.data; ep.y_sn = Y.stride[0]; ep.y_sh = Y.stride[2]; ep.y_sw = Y.stride[3];
+        ep.oy0 = a.oy0; ep.ox0 = a.ox0; ep.osy = a.osy; ep.osx = a.osx;
+        ep.bias = bias; ep.bias_mod = 0;
+        ep.R = R.data; ep.r_sn = R.stride[0]; ep.r_sh = R.stride[2]; ep.r_sw = R.stride[3];
+        ep.res_scale = res_scale; ep.act = act; ep.slope = slope; ep.dtype = dtype;
+        e = launch_epilogue(ep, s);
+        if (e) return hip_check(e, "halo epilogue");
+      }
       continue;
     }
     if (a.nunits > 0) {
@@ -453,7 +507,8 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     if (e) return hip_check(e, "igemm");
     if (a.ksplit > 1) {
       EpiArgs ep;
-      ep.ws = a.ws; ep.M = a.M; ep.Nout = a.Nout; ep.JH = a.JH; ep.JW = a.JW;
+      memset(&ep, 0, sizeof(ep));
+      ep.ws = a.ws; ep.nslices = 1; ep.slice = 0; ep.M = a.M; ep.Nout = a.Nout; ep.JH = a.JH; ep.JW = a.JW;
       ep.Y = a.Y; ep.y_sn = a.y_sn; ep.y_sh = a.y_sh; ep.y_sw = a.y_sw;
       ep.oy0 = a.oy0; ep.ox0 = a.ox0; ep.osy = a.osy; ep.osx = a.osx;
       ep.bias = bias; ep.bias_mod = bias_mod;
@@ -564,19 +619,40 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   a.div_phpw.init(a.PH * a.PW);
   // pipelined DMA kernel when both operands are 16-byte aligned channels-last rows
   if (a.vec_p && a.vec_q) {
-    static const int cand[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
-    int bm = 0, bn = 0;
-    int64_t best = -1;
-    for (auto& c : cand) {
-      // padded MACs, small tiles charged 15% for their lower operand reuse
-      int64_t cost = (int64_t)rup(a.Ca, c[0]) * rup(a.Cb, c[1]) * ((c[0] == 64 || c[1] == 64) ? 115 : 100);
-      if (best < 0 || cost < best) { best = cost; bm = c[0]; bn = c[1]; }
-    }
+    // non-composite: columns flattened over taps (b' = tap * rup(Cb, 8) + b), so channel
+    // counts like 75 / 206 waste at most 7 columns per tap instead of a tile remainder
+    a.bflat = comp ? 0 : 1;
+    a.cbp = (int)rup(a.Cb, 8);
+    const int64_t ncols = a.bflat ? (int64_t)a.ntaps * a.cbp : a.Cb;
+    const int ngrid = a.bflat ? 1 : a.ntaps;
+    // Tile and pixel-split choice from a measured cost model (tools/bench_layers.py
+    // sweeps): a block costs (k-tiles + O) k-tile times, O = 23 with the atomic epilogue
+    // (8 without a split); blocks run in rounds of (CUs x blocks per CU); work per
+    // k-tile scales with the tile area, 64-wide tiles pay 15% for lower operand reuse.
+    static const int cand[5][3] = {{256, 128, 1}, {128, 128, 1}, {128, 64, 2}, {64, 128, 2}, {64, 64, 2}};
     const int kp = d->dtype == TPG_BF16 ? 64 : 32;
-    const int tiles = cdiv(a.Ca, bm) * cdiv(a.Cb, bn) * a.ntaps;
-    int ks = std::max(1, cdiv(2048, tiles));
-    ks = std::min(ks, std::max(1, a.npix / (kp * 8)));
-    a.pix_per_split = (int)rup(cdiv(a.npix, ks), kp);
+    const int nkt = cdiv(a.npix, kp);
+    int bm = 0, bn = 0, bks = 1;
+    double best = -1.0;
+    for (auto& c : cand) {
+      const int64_t tiles = (int64_t)cdiv(a.Ca, c[0]) * ((ncols + c[1] - 1) / c[1]) * ngrid;
+      const double area = (double)c[0] * c[1] / 32768.0 * ((c[0] == 64 || c[1] == 64) ? 1.15 : 1.0);
+      const int64_t slots = 256 * (int64_t)c[2];
+      for (int ks = 1; ks <= std::min(nkt, 256); ++ks) {
+        const int kpb = cdiv(nkt, ks);
+        if (ks > 1 && cdiv(nkt, kpb) != ks) continue;  // same per-block work as a smaller ks
+        const int64_t rounds = (tiles * ks + slots - 1) / slots;
+        const double t = (double)rounds * (kpb + (ks > 1 ? 23 : 8)) * area;
+        if (best < 0 || t < best * 0.999) { best = t; bm = c[0]; bn = c[1]; bks = ks; }
+      }
+    }
+    if (const char* f = getenv("TPG_WGRAD_FORCE")) {  // tuning hook: "bm,bn,ks"
+      int fm = 0, fn = 0, fk = 0;
+      if (sscanf(f, "%d,%d,%d", &fm, &fn, &fk) == 3 && wgrad2_cfg(fm, fn) >= 0 && fk >= 1) {
+        bm = fm; bn = fn; bks = std::min(fk, nkt);
+      }
+    }
+    a.pix_per_split = (int)rup(cdiv(a.npix, bks), kp);
     a.ksplit = cdiv(a.npix, a.pix_per_split);
     const int es = esize(d->dtype);
     auto extent = [&](const tpg_tensor& t, int n, int h, int w, int c) -> int64_t {

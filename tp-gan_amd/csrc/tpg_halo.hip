@@ -5,15 +5,17 @@
 // gradient at any stride and the ConvTranspose2d forward (one launch per parity class,
 // SURVEY.md §7 step 5).  That is > 90 % of the G+D train-step MACs of the fwd + dgrad passes.
 //
-// Block = a TH x TW tile of output (sub-grid) pixels of one image x BN output channels,
-// 8 waves.  K loop: for each 64-byte channel step (bf16: 32 ch, f32: 16 ch)
+// Block = 256 output (sub-grid) pixels x BN output channels, 8 waves: one TH x TW tile of
+// one image, or IMG whole small images (8x8, 10x10, 5x5 ... maps) side by side.  K loop: for each 64-byte channel step (bf16: 32 ch, f32: 16 ch)
 //   - the input halo (TH + dy range) x (TW + dx range) pixels x 64 B is gathered ONCE
 //     into LDS (zero / reflected outside the image) and reused by all taps;
 //   - for each tap the [BN][64 B] weight slice (packed contiguous, pre-swizzled) is staged
 //     through a second LDS double buffer, and every wave runs MREP x NREP MFMAs with A
 //     fragments read from the halo at the tap's (dy, dx) shift.
-// Next step's halo and next tap's weights are prefetched into registers while the current
-// tap computes (software pipeline, one barrier per tap).
+// Next step's halo is prefetched into registers and the weights two taps ahead are in
+// flight by LDS-DMA while the current tap computes (software pipeline, one barrier per tap).
+// Small maps have too few tiles to fill 256 CUs: the k-steps are then split over grid.z and
+// each split writes an fp32 partial slice, summed by the epilogue kernel (no atomics).
 //
 // LDS images use 64-byte pixel rows; the 16-byte chunk g of row p is stored at
 // g ^ (((p >> 2) & 1) << 1), which makes the ds_read_b128 fragment reads of both
@@ -58,59 +60,67 @@ __device__ __forceinline__ int h_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-template <bool BF, int TH, int TW, int KMAX, int BN, int WM, int WN>
+template <bool BF, int HL, int BN, int WM, int WN>
 __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   using E = typename std::conditional<BF, __bf16, float>::type;
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
   constexpr int KS = 4 * EPC;                // channels per 64-byte step
-  constexpr int BM = TH * TW;
-  constexpr int HMAX = (TH + KMAX - 1) * (TW + KMAX - 1);  // halo pixels for KMAX x KMAX taps
-  constexpr int HL = (HMAX * 4 + 511) / 512; // halo chunks staged per thread
+  constexpr int BM = 256;                    // output rows per block (IMG sub-tiles)
   constexpr int BNL = halo_bnl(BN);          // weight rows per LDS slot (multiple of 128)
   constexpr int GL = BNL / 128;              // 1 KiB LDS-DMA pieces per wave per step
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MREP = WTM / 16, NREP = WTN / 16;
   static_assert(WM * WN == 8, "8 waves");
   static_assert(MREP * 16 * WM == BM && NREP * 16 * WN == BN, "tile");
-  static_assert(TW % 16 == 0, "tile rows must hold whole 16-pixel fragments");
 
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
-  u32x4* halo = lds;                                   // [2][HMAX][4]
-  u32x4* wts = lds + 2 * HMAX * 4;                     // [3][BNL][4] ring
+  const int hcap = p.hcap;
+  u32x4* halo = lds;                                   // [2][hcap][4]
+  u32x4* wts = lds + 2 * hcap * 4;                     // [3][BNL][4] ring
   int* s_toff = reinterpret_cast<int*>(wts + 3 * BNL * 4);  // [TPG_MAX_TAPS]
 
   const int tid = threadIdx.x;
   if (tid < TPG_MAX_TAPS) s_toff[tid] = p.toff[tid];
-  const int HW = p.HW, HP = p.HH * HW;
-  const int tiles = p.tiles_h * p.tiles_w;
-  const int nimg = blockIdx.x / tiles;
-  const int trem = blockIdx.x - nimg * tiles;
-  const int th = trem / p.tiles_w;
-  const int j0 = th * TH, i0 = (trem - th * p.tiles_w) * TW;
+  const int TH = p.TH, TW = p.TW, IMG = p.IMG, SH = p.SH, SW = p.SW;
+  const int THW = TH * TW;
+  const int HW = p.HW, HP = p.HH * HW;                 // halo pixels of one sub-tile
+  const int tiles = p.tiles_h * p.tiles_w, tiles_w = p.tiles_w;
+  const int ntot = p.N * tiles;                        // sub-tiles in the grid
+  const int st0 = blockIdx.x * IMG;
   const int n0 = blockIdx.y * BN;
-  const E* Ag = reinterpret_cast<const E*>(p.A) + (int64_t)nimg * p.a_sn;
+  const int z = blockIdx.z;
+  const int ks0 = z * p.kps;
+  const int nks = min(p.nks, ks0 + p.kps) - ks0;
+  const E* Ag = reinterpret_cast<const E*>(p.A);
   const int wave = tid >> 6, lane = tid & 63;
   // packed weights: Wp[step][ntile][BNL][4 chunks]; this wave streams GL KiB of each slice
-  const char* wsrc = reinterpret_cast<const char*>(p.Wp) + (int64_t)blockIdx.y * BNL * 64 +
-                     (wave * GL * 1024 + lane * 16);
   const int64_t wstep = (int64_t)p.ntiles * BNL * 64;
+  const char* wsrc = reinterpret_cast<const char*>(p.Wp) + (int64_t)ks0 * p.ntaps * wstep +
+                     (int64_t)blockIdx.y * BNL * 64 + (wave * GL * 1024 + lane * 16);
 
-  // ---- per-thread halo slots (fixed across k-steps): element offset inside the image
-  // (negative = outside -> zero)
+  // ---- per-thread halo slots (fixed across k-steps): element offset from A (absolute,
+  // < 2^31 by the planner), negative = outside the image or a dead sub-tile -> zero
   int hoff[HL];
 #pragma unroll
   for (int q = 0; q < HL; ++q) {
     const int idx = tid + 512 * q;
     const int hp = idx >> 2, ch = idx & 3;
     hoff[q] = -1;
-    if (hp < HP) {
-      const int hy = hp / HW, hx = hp - (hp / HW) * HW;
-      int gy = j0 + p.dymin + hy, gx = i0 + p.dxmin + hx;
-      if (p.pad_mode) { gy = h_refl(gy, p.A_H); gx = h_refl(gx, p.A_W); }
-      if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W)
-        hoff[q] = gy * (int)p.a_sh + gx * (int)p.a_sw + ch * EPC;
+    if (hp < IMG * HP) {
+      const int sub = hp / HP, hl = hp - sub * HP;
+      const int st = st0 + sub;
+      if (st < ntot) {
+        const int nimg = st / tiles, trem = st - nimg * tiles;
+        const int ty = trem / tiles_w, tx = trem - ty * tiles_w;
+        const int hy = hl / HW, hx = hl - hy * HW;
+        int gy = ty * TH * SH + p.dymin + hy, gx = tx * TW * SW + p.dxmin + hx;
+        if (p.pad_mode) { gy = h_refl(gy, p.A_H); gx = h_refl(gx, p.A_W); }
+        if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W)
+          hoff[q] = (int)((int64_t)nimg * p.a_sn + gy * p.a_sh + gx * p.a_sw) + ch * EPC;
+      }
     }
   }
+  const int HPT = IMG * HP;
 
   // Halo chunks are loaded raw (clamped address, unconditional 16-byte load) and masked
   // only when written to LDS a whole k-step later.  (vec-only kernel: the planner sends
@@ -118,7 +128,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   u32x4 hreg[HL];
   int hc = 0;
   auto load_halo = [&](int ks) {
-    const int cbase = ks * KS;
+    const int cbase = (ks0 + ks) * KS;
     hc = cbase + (tid & 3) * EPC;
 #pragma unroll
     for (int q = 0; q < HL; ++q) {
@@ -127,14 +137,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     }
   };
   auto store_halo = [&](int buf) {
-    u32x4* H = halo + buf * HMAX * 4;
+    u32x4* H = halo + buf * hcap * 4;
 #pragma unroll
     for (int q = 0; q < HL; ++q) {
       const int idx = tid + 512 * q;
       const int hp = idx >> 2;
       u32x4 v = mask_chunk4<EPC>(hreg[q], hc, p.C);
       if (hoff[q] < 0) v = u32x4{0u, 0u, 0u, 0u};
-      if (hp < HP) H[hp * 4 + ((idx & 3) ^ hswz(hp))] = v;
+      if (hp < HPT) H[hp * 4 + ((idx & 3) ^ hswz(hp))] = v;
     }
   };
   // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
@@ -153,8 +163,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 #pragma unroll
   for (int m = 0; m < MREP; ++m) {
     const int q = wm * WTM + m * 16 + l16;
-    const int ty = q / TW, tx = q - (q / TW) * TW;
-    hbase[m] = ty * HW + tx;
+    const int sub = q / THW, rem = q - sub * THW;
+    const int ty = rem / TW, tx = rem - ty * TW;
+    hbase[m] = sub < IMG ? sub * HP + ty * SH * HW + tx * SW : 0;  // dead rows read row 0
   }
   f32x4 acc[MREP][NREP];
 #pragma unroll
@@ -163,7 +174,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int hbuf, int wslot, int toff) {
-    const u32x4* H = halo + hbuf * HMAX * 4;
+    const u32x4* H = halo + hbuf * hcap * 4;
     const u32x4* Wl = wts + wslot * BNL * 4;
     u32x4 af[MREP];
 #pragma unroll
@@ -199,7 +210,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   //   end of s   : at t == ntaps-1 write the next halo to LDS; s_waitcnt vmcnt(GL)
   //                retires step s+1's DMA (issued during s-1) while step s+2's stays in
   //                flight; lgkmcnt(0); s_barrier.  Step s+1 then reads what was retired.
-  const int nks = p.nks, ntaps = p.ntaps;
+  const int ntaps = p.ntaps;
   const int total = nks * ntaps;
   __syncthreads();  // tap table
   if (total > 0) {
@@ -227,17 +238,32 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
   }
 
-  // ---- epilogue
+  // ---- epilogue: fused bias / residual / activation store, or an fp32 partial slice
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
+  float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
 #pragma unroll
   for (int m = 0; m < MREP; ++m) {
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int q = wm * WTM + m * 16 + 4 * g + reg;
-      const int ty = q / TW, tx = q - (q / TW) * TW;
-      const int j = j0 + ty, i = i0 + tx;
+      const int sub = q / THW, rem = q - sub * THW;
+      const int st = st0 + sub;
+      if (sub >= IMG || st >= ntot) continue;
+      const int nimg = st / tiles, trem = st - nimg * tiles;
+      const int tty = trem / tiles_w, ttx = trem - tty * tiles_w;
+      const int ty = rem / TW, tx = rem - ty * TW;
+      const int j = tty * TH + ty, i = ttx * TW + tx;
       if (j >= p.JH || i >= p.JW) continue;
+      if (W) {
+        float* wr = W + ((int64_t)(nimg * p.JH + j) * p.JW + i) * p.Nout;
+#pragma unroll
+        for (int nr = 0; nr < NREP; ++nr) {
+          const int col = n0 + wn * WTN + nr * 16 + l16;
+          if (col < p.Nout) wr[col] = acc[m][nr][reg];
+        }
+        continue;
+      }
       const int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
       const int64_t yoff = (int64_t)nimg * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
       const int64_t roff = (int64_t)nimg * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
@@ -254,47 +280,46 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   }
 }
 
-// {id, TH, TW, KMAX, BN, WM, WN}; id = 15 * (TW == 16) + 5 * kclass + bn index
-#define TPG_HALO_BN(X, ID, TH, TW, K)  \
-  X(ID + 0, TH, TW, K, 32, 8, 1)       \
-  X(ID + 1, TH, TW, K, 64, 8, 1)       \
-  X(ID + 2, TH, TW, K, 96, 8, 1)       \
-  X(ID + 3, TH, TW, K, 128, 4, 2)      \
-  X(ID + 4, TH, TW, K, 224, 4, 2)
-#define TPG_HALO_CFGS(X)               \
-  TPG_HALO_BN(X, 0, 8, 32, 3)          \
-  TPG_HALO_BN(X, 5, 8, 32, 5)          \
-  TPG_HALO_BN(X, 10, 8, 32, 7)         \
-  TPG_HALO_BN(X, 15, 16, 16, 3)        \
-  TPG_HALO_BN(X, 20, 16, 16, 5)        \
-  TPG_HALO_BN(X, 25, 16, 16, 7)
+// {id, HL, BN, WM, WN}; id = 5 * (HL - 3) + bn index.  HL = halo chunks per thread:
+// the halo buffer holds up to HL*128 pixels.
+#define TPG_HALO_BN(X, ID, HL)  \
+  X(ID + 0, HL, 32, 8, 1)       \
+  X(ID + 1, HL, 64, 8, 1)       \
+  X(ID + 2, HL, 96, 8, 1)       \
+  X(ID + 3, HL, 128, 4, 2)      \
+  X(ID + 4, HL, 224, 4, 2)
+#define TPG_HALO_CFGS(X)        \
+  TPG_HALO_BN(X, 0, 3)          \
+  TPG_HALO_BN(X, 5, 4)          \
+  TPG_HALO_BN(X, 10, 5)
 
-int halo_cfg(int tw, int kspan, int bn) {
+int halo_cfg(int hl, int bn) {
   const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : -1;
-  if (bi < 0 || kspan > 7 || (tw != 16 && tw != 32)) return -1;
-  const int kc = kspan <= 3 ? 0 : kspan <= 5 ? 1 : 2;
-  return (tw == 16 ? 15 : 0) + 5 * kc + bi;
+  if (bi < 0 || hl < 3 || hl > 5) return -1;
+  return 5 * (hl - 3) + bi;
 }
 
-static size_t halo_lds_bytes(int th, int tw, int k, int bn) {
-  return (size_t)(2 * (th + k - 1) * (tw + k - 1) * 4 + 3 * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
+size_t halo_lds_bytes(int hcap, int bn) {
+  return (size_t)(2 * hcap * 4 + 3 * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
 }
 
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s) {
-  dim3 grid(a.N * a.tiles_h * a.tiles_w, a.ntiles);
-#define X(id, TH_, TW_, K_, BN_, WM_, WN_)                                                                    \
+  dim3 grid((a.N * a.tiles_h * a.tiles_w + a.IMG - 1) / a.IMG, a.ntiles, a.ksplit);
+  const size_t lds = halo_lds_bytes(a.hcap, a.BN);
+#define X(id, HL_, BN_, WM_, WN_)                                                                             \
   if (cfg == (id)) {                                                                                          \
-    const size_t lds = halo_lds_bytes(TH_, TW_, K_, BN_);                                                     \
+    if (a.hcap > HL_ * 128) return -1;                                                                        \
+    const int maxl = (int)halo_lds_bytes(HL_ * 128, BN_);                                                     \
     if (dtype == 1) {                                                                                         \
-      auto k = halo_kernel<true, TH_, TW_, K_, BN_, WM_, WN_>;                                                \
+      auto k = halo_kernel<true, HL_, BN_, WM_, WN_>;                                                         \
       static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                                    (int)lds), true);                                         \
+                                                    maxl), true);                                             \
       (void)once;                                                                                             \
       hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                      \
     } else {                                                                                                  \
-      auto k = halo_kernel<false, TH_, TW_, K_, BN_, WM_, WN_>;                                               \
+      auto k = halo_kernel<false, HL_, BN_, WM_, WN_>;                                                        \
       static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                                    (int)lds), true);                                         \
+                                                    maxl), true);                                             \
       (void)once;                                                                                             \
       hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                      \
     }                                                                                                         \

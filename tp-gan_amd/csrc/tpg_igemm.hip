@@ -263,24 +263,44 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
   }
 }
 
-template <typename E>
+// Split-K finalize: v = sum of the partial slices (+ bias, + residual, activation).
+// V columns per thread (4 when Nout % 4 == 0: 16-byte slice reads).
+template <typename E, int V>
 __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs p) {
-  const int64_t total = (int64_t)p.M * p.Nout;
+  const int64_t total = (int64_t)p.M * p.Nout / V;
   const int JHJW = p.JH * p.JW;
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int row = (int)(idx / p.Nout);
-    int col = (int)(idx - (int64_t)row * p.Nout);
+    const int64_t e0 = idx * V;
+    int row = (int)(e0 / p.Nout);
+    int col = (int)(e0 - (int64_t)row * p.Nout);
     int n = row / JHJW;
     int rem = row - n * JHJW;
     int j = rem / p.JW, i = rem - j * p.JW;
     int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
-    float v = p.ws[idx];
-    if (p.bias) v += p.bias[p.bias_mod ? col % p.bias_mod : col];
-    if (R) v += p.res_scale * ld_f(R + (int64_t)n * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw + col);
-    st_f(Y + (int64_t)n * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw + col, act_apply(v, p.act, p.slope));
+    float v[V];
+    if constexpr (V == 4) {
+      float4 a = *reinterpret_cast<const float4*>(p.ws + e0);
+      for (int z = 1; z < p.nslices; ++z) {
+        const float4 b = *reinterpret_cast<const float4*>(p.ws + z * p.slice + e0);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else {
+      v[0] = p.ws[e0];
+      for (int z = 1; z < p.nslices; ++z) v[0] += p.ws[z * p.slice + e0];
+    }
+    const int64_t yo = (int64_t)n * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw + col;
+    const int64_t ro = (int64_t)n * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw + col;
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      float x = v[u];
+      if (p.bias) x += p.bias[p.bias_mod ? (col + u) % p.bias_mod : col + u];
+      if (R) x += p.res_scale * ld_f(R + ro + u);
+      st_f(Y + yo + u, act_apply(x, p.act, p.slope));
+    }
   }
 }
 
@@ -321,11 +341,17 @@ int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s) {
 }
 
 int launch_epilogue(const EpiArgs& a, hipStream_t s) {
-  int64_t total = (int64_t)a.M * a.Nout;
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  const bool v4 = a.Nout % 4 == 0 && ((uintptr_t)a.ws % 16) == 0 && a.slice % 4 == 0;
+  int64_t total = (int64_t)a.M * a.Nout / (v4 ? 4 : 1);
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (blocks < 1) blocks = 1;
-  if (a.dtype == 1) hipLaunchKernelGGL(epilogue_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(epilogue_kernel<float>, dim3(blocks), dim3(256), 0, s, a);
+  if (a.dtype == 1) {
+    if (v4) hipLaunchKernelGGL((epilogue_kernel<__bf16, 4>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((epilogue_kernel<__bf16, 1>), dim3(blocks), dim3(256), 0, s, a);
+  } else {
+    if (v4) hipLaunchKernelGGL((epilogue_kernel<float, 4>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((epilogue_kernel<float, 1>), dim3(blocks), dim3(256), 0, s, a);
+  }
   return (int)hipGetLastError();
 }
 

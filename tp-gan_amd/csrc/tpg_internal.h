@@ -99,6 +99,7 @@ struct WgradArgs {
   FastDiv div_pw, div_phpw;
   int8_t dy[TPG_MAX_TAPS], dx[TPG_MAX_TAPS], tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
   int p_bytes, q_bytes;       // buffer extents for the DMA kernel (out-of-range reads -> 0)
+  int bflat, cbp;             // wgrad2 tap-flattened columns: b' = tap * cbp + b, cbp = rup(Cb, 8)
 };
 typedef WgradArgs Wgrad2Args;
 
@@ -117,8 +118,10 @@ struct PackArgs {
   int8_t tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
 };
 
-struct EpiArgs {               // split-K finalize
+struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [+ res])
   const float* ws;
+  int nslices;                // number of partial slices (1 for atomically accumulated ws)
+  int64_t slice;              // elements per slice (M * Nout)
   int M, Nout, JH, JW;
   void* Y;
   int64_t y_sn, y_sh, y_sw;
@@ -134,16 +137,22 @@ struct EpiArgs {               // split-K finalize
 };
 
 // ---------------------------------------------------------------- halo direct conv ----
-// Stride-1 (sub-)grid conv: output (sub-grid) pixel (j, i) reads A at (j + dy[t], i + dx[t]).
+// (Sub-)grid conv: output (sub-grid) pixel (j, i) reads A at (j*SH + dy[t], i*SW + dx[t]).
+// A block owns IMG sub-tiles of TH x TW output pixels (IMG > 1 only for whole-image tiles of
+// small maps), i.e. up to 256 rows, and k-steps [z*kps, (z+1)*kps) of its split z.
 struct HaloArgs {
   const void* A;
   int64_t a_sn, a_sh, a_sw;
   int A_H, A_W, C;
   int nks;                    // 64-byte channel steps = ceil(C / KS)
   int ntaps;
-  int dymin, dxmin, HH, HW;   // halo = (TH + dy range) x (TW + dx range)
+  int dymin, dxmin, HH, HW;   // halo of one sub-tile = HH x HW pixels
   int pad_mode, vec_ok;        // vec_ok: 16-byte loads of whole chunks stay inside each pixel row
   int N, JH, JW, tiles_h, tiles_w;
+  int TH, TW, IMG, SH, SW;    // sub-tile shape, sub-tiles per block, A-grid stride of the taps
+  int hcap;                   // halo pixels per LDS buffer (>= IMG*HH*HW)
+  int ksplit, kps;            // split over k-steps (grid.z); > 1 -> fp32 partials into ws
+  float* ws;                  // [ksplit][N*JH*JW][Nout] partial slices (class-local rows)
   const void* Wp;             // [nks*ntaps][ntiles][rup(BN,128)][64 B], rows pre-swizzled
   int ntiles, BN, Nout;
   void* Y;
@@ -169,7 +178,8 @@ int launch_pack(const PackArgs& a, hipStream_t s);
 int wgrad2_cfg(int bm, int bn);
 int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s);
 int launch_epilogue(const EpiArgs& a, hipStream_t s);
-int halo_cfg(int tw, int kspan, int bn);
+int halo_cfg(int hl, int bn);
+size_t halo_lds_bytes(int hcap, int bn);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);

@@ -47,7 +47,7 @@ __device__ __forceinline__ int w2_swz(int row) {
   }
 }
 
-template <bool BF, int BM, int BN, int WM, int WN>
+template <bool BF, int BM, int BN, int WM, int WN, bool FLAT>
 __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
   using E = typename std::conditional<BF, __bf16, float>::type;
   constexpr int ES = sizeof(E);
@@ -65,11 +65,19 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [3][STAGE]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // 1-D grid, logical block = (tile, tap, split), tile fastest.  Physical block b runs on
+  // XCD b % 8; each XCD is handed a contiguous range of logical blocks, so the tiles that
+  // share a pixel range (same dY rows, X rows shifted by the taps) meet in one L2.
   const int nta = (p.Ca + BM - 1) / BM;
-  const int ta = blockIdx.x % nta, tb = blockIdx.x / nta;
+  const int ntb = ((FLAT ? p.ntaps * p.cbp : p.Cb) + BN - 1) / BN;
+  const int nblk = gridDim.x, full = nblk & ~7;
+  const int bid = blockIdx.x;
+  const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
+  const int tile = L % (nta * ntb), rest = L / (nta * ntb);
+  const int ta = tile % nta, tb = tile / nta;
   const int a0 = ta * BM, b0 = tb * BN;
-  const int tap = blockIdx.y;
-  const int pbeg = blockIdx.z * p.pix_per_split;
+  const int tap = FLAT ? 0 : rest % p.ntaps;
+  const int pbeg = (FLAT ? rest : rest / p.ntaps) * p.pix_per_split;
   const int pend = min(p.npix, pbeg + p.pix_per_split);
   const int nkt = (pend - pbeg + KP - 1) / KP;
   const int dy = p.dy[tap], dx = p.dx[tap];
@@ -80,6 +88,25 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
   const int Ca = p.Ca, Cb = p.Cb;
   const int64_t psn = p.p_sn, psh = p.p_sh, psw = p.p_sw, qsn = p.q_sn, qsh_ = p.q_sh, qsw_ = p.q_sw;
 
+  // FLAT: B columns are b' = tap * cbp + b over all taps (a 16-byte chunk never straddles
+  // taps since cbp % 8 == 0); each lane's chunk, hence its tap, is fixed per DMA piece.
+  int ldy[GB], ldx[GB], lcb[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int o = (wave * GB + j) * 1024 + lane * 16;
+    const int row = o / RBB, pc = (o % RBB) / 16;
+    const int lc = pc ^ w2_swz<BF, RBB>(row);
+    const int col = b0 + lc * EPC;
+    if constexpr (FLAT) {
+      const int t = col / p.cbp;
+      const int tc = t < p.ntaps ? t : 0;
+      ldy[j] = p.dy[tc];
+      ldx[j] = p.dx[tc];
+      lcb[j] = t < p.ntaps ? col - t * p.cbp : (1 << 30);  // past the last tap -> zero
+    } else {
+      ldy[j] = dy; ldx[j] = dx; lcb[j] = col;
+    }
+  }
   const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.P), 0, p.p_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Q), 0, p.q_bytes, 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
@@ -108,17 +135,16 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const int o = (wave * GB + j) * 1024 + lane * 16;
-      const int row = o / RBB, pc = (o % RBB) / 16;
-      const int lc = pc ^ w2_swz<BF, RBB>(row);
+      const int row = o / RBB;
       const int pix = p0 + row;
-      const int c = b0 + lc * EPC;
+      const int c = lcb[j];
       unsigned off = OOB;
       {
         const int n = dv_phpw.div(pix), rem = pix - n * PHPW;
         const int py = dv_pw.div(rem), px = rem - py * PW;
-        int qy = py * qsh + dy, qx = px * qsw + dx;
+        int qy = py * qsh + ldy[j], qx = px * qsw + ldx[j];
         if (pad_mode) { qy = w2_refl(qy, QH); qx = w2_refl(qx, QW); }
-        const bool ok = pix < pend && c < Cb && (unsigned)qy < (unsigned)QH && (unsigned)qx < (unsigned)QW;
+        const bool ok = pix < pend && c < (FLAT ? p.cbp : Cb) && (unsigned)qy < (unsigned)QH && (unsigned)qx < (unsigned)QW;
         const unsigned o2 = (unsigned)((n * qsn + qy * qsh_ + qx * qsw_ + c) * ES);
         off = ok ? o2 : OOB;
       }
@@ -227,7 +253,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
   }
 #undef W2_WAIT_BARRIER
 
-  // ---- epilogue: fp32 atomics into dW (C/D layout: col = lane&15 -> b, row = 4g+reg -> a)
+  // ---- epilogue: fp32 atomics into dW (plain read-add-write without a pixel split) (C/D layout: col = lane&15 -> b, row = 4g+reg -> a)
   const int r_tap = p.tr[tap], s_tap = p.ts[tap];
 #pragma unroll
   for (int m = 0; m < MREP; ++m)
@@ -238,15 +264,24 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 #pragma unroll
       for (int n = 0; n < NREP; ++n) {
         const int bq = b0 + wn * WTN + n * 16 + l16;
-        if (bq >= p.Cb) continue;
         int r = r_tap, s = s_tap, b = bq;
-        if (p.bcomp) {
+        if constexpr (FLAT) {
+          const int t = bq / p.cbp;
+          b = bq - t * p.cbp;
+          if (t >= p.ntaps || b >= p.Cb) continue;
+          r = p.tr[t];
+          s = p.ts[t];
+        } else if (bq >= p.Cb) {
+          continue;
+        } else if (p.bcomp) {
           const int rs = bq / p.comp_cb;
           b = bq - rs * p.comp_cb;
           r = rs / p.comp_kw;
           s = rs - r * p.comp_kw;
         }
-        atomicAdd(p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss, acc[m][n][reg]);
+        float* dst = p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss;
+        if (p.ksplit == 1) *dst += acc[m][n][reg];  // sole owner of this dW element
+        else atomicAdd(dst, acc[m][n][reg]);
       }
     }
 }
@@ -266,19 +301,21 @@ int wgrad2_cfg(int bm, int bn) {
   return -1;
 }
 
-int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s) {
-  dim3 grid(((a.Ca + bm - 1) / bm) * ((a.Cb + bn - 1) / bn), a.ntaps, a.ksplit);
+template <bool FLAT>
+static int launch_wgrad2_t(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s) {
+  const int ncols = FLAT ? a.ntaps * a.cbp : a.Cb;
+  dim3 grid(((a.Ca + bm - 1) / bm) * ((ncols + bn - 1) / bn) * (FLAT ? 1 : a.ntaps) * a.ksplit);
 #define X(id, BM_, BN_, WM_, WN_)                                                                       \
   if (cfg == (id)) {                                                                                    \
     if (dtype == 1) {                                                                                   \
-      auto k = wgrad2_kernel<true, BM_, BN_, WM_, WN_>;                                                 \
+      auto k = wgrad2_kernel<true, BM_, BN_, WM_, WN_, FLAT>;                                           \
       const size_t lds = 3 * 64 * (BM_ + BN_) * 2;                                                      \
       static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                                     (int)lds), true);                                   \
       (void)once;                                                                                       \
       hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                \
     } else {                                                                                            \
-      auto k = wgrad2_kernel<false, BM_, BN_, WM_, WN_>;                                                \
+      auto k = wgrad2_kernel<false, BM_, BN_, WM_, WN_, FLAT>;                                          \
       const size_t lds = 3 * 32 * (BM_ + BN_) * 4;                                                      \
       static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                                     (int)lds), true);                                   \
@@ -290,6 +327,10 @@ int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipSt
   TPG_WGRAD2_CFGS(X)
 #undef X
   return -1;
+}
+
+int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s) {
+  return a.bflat ? launch_wgrad2_t<true>(a, dtype, cfg, bm, bn, s) : launch_wgrad2_t<false>(a, dtype, cfg, bm, bn, s);
 }
 
 }  // namespace tpg

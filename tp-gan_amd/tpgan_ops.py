@@ -45,11 +45,18 @@ def _probe_begin(d, which):
     return e0
 
 
-def _probe_end(e0, d):
+def _probe_end(e0, d, which=""):
     if e0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        PROBE["events"].append((e0, e1, _conv_flops(d)))
+        work = _conv_flops(d) if which != "actb" else 6 * d.n * d.out_h * d.out_w * d.out_c  # bytes for act'
+        PROBE["events"].append((e0, e1, work, which, desc_key(d)))
+
+
+def desc_key(d):
+    """Short human-readable shape of a conv descriptor (per-layer traces)."""
+    return "%s%dx%d s%d n%d %dx%dx%d->%dx%dx%d" % ("T" if d.transposed else "", d.kh, d.kw, d.stride_h, d.n,
+                                                 d.in_c, d.in_h, d.in_w, d.out_c, d.out_h, d.out_w)
 
 
 def _conv_flops(d):
@@ -69,6 +76,19 @@ def compute_dtype(dt):
 
 def get_compute_dtype():
     return _DTYPE[-1]
+
+
+# Run the Generator's four local pathways on side streams (D_and_G_model.Generator).
+MULTISTREAM = True
+_SIDE = {}
+
+
+def side_streams(device, n):
+    """n persistent side HIP streams of `device` (created once)."""
+    key = (torch.device(device).index, n)
+    if key not in _SIDE:
+        _SIDE[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+    return _SIDE[key]
 
 
 def _ceil8(c):
@@ -165,7 +185,7 @@ class _ConvAct(torch.autograd.Function):
     saved input and output, never the pre-activation)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale):
+    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam):
         lib = load()
         dtype = get_compute_dtype()
         ctx.in_dtype = x.dtype
@@ -191,11 +211,13 @@ class _ConvAct(torch.autograd.Function):
         e0 = _probe_begin(d, "fwd")
         check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bias.data_ptr() if bias is not None else None,
                                  tt(res), tt(_fix_c1(y)), ws.data_ptr(), ws.numel(), stream_ptr()))
-        _probe_end(e0, d)
+        _probe_end(e0, d, "fwd")
         ctx.save_for_backward(x, weight, y)
         ctx.geom, ctx.act, ctx.slope, ctx.res_scale = geom, act, slope, res_scale
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
         ctx.d = d
+        ctx.wparam = wparam if wparam is not None else weight
+        ctx.bparam = bias
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.x_dtype = x.dtype
         return y
@@ -208,9 +230,17 @@ class _ConvAct(torch.autograd.Function):
         dtype = y.dtype
         n, cout, oh, ow = y.shape
         g = new_act(n, cout, oh, ow, dtype, y.device)
-        dbias = torch.zeros(cout, dtype=torch.float32, device=y.device) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        dbias = None
+        fused_b = False
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            fused_b = _fused_target(ctx.bparam) is not None
+            dbias = ctx.bparam.grad if fused_b else torch.zeros(cout, dtype=torch.float32, device=y.device)
+        e0 = _probe_begin(d, "actb")
         check(lib.tpg_act_bwd(n, cout, oh, ow, ctx.act, ctx.slope, tt(gy), tt(y), tt(_fix_c1(g)),
                               dbias.data_ptr() if dbias is not None else None, stream_ptr()))
+        _probe_end(e0, d, "actb")
+        if fused_b:
+            dbias = None  # accumulated straight into bias.grad
         g = _fix_c1(g)
         dx = dw = dres = None
         wv = weight if weight.dtype == torch.float32 else weight.float()
@@ -221,37 +251,54 @@ class _ConvAct(torch.autograd.Function):
             e0 = _probe_begin(d, "dgrad")
             check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(_fix_c1(dx)), ws.data_ptr(), ws.numel(),
                                           stream_ptr()))
-            _probe_end(e0, d)
+            _probe_end(e0, d, "dgrad")
             if dx.dtype != ctx.in_dtype:
                 dx = dx.to(ctx.in_dtype)
         if ctx.needs_input_grad[1]:
-            dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
-            if weight.dim() == 4:
-                dw = dw.contiguous(memory_format=torch.channels_last) if weight.is_contiguous(
-                    memory_format=torch.channels_last) else dw
-            dwv = dw if dw.dim() == 4 else dw.view(weight.shape[0], -1, d.kh, d.kw)
+            tgt = _fused_target(ctx.wparam)
+            if tgt is not None:  # dW accumulates straight into the flat gradient buffer
+                dw = None
+                dwv = tgt if tgt.shape == weight.shape else tgt.view(weight.shape)
+            else:
+                dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
+                if weight.dim() == 4 and weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous(memory_format=torch.channels_last)
+                dwv = dw
             FLOPS["wgrad"] += _conv_flops(d)
             e0 = _probe_begin(d, "wgrad")
             check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dwv), None, 0, stream_ptr()))
-            _probe_end(e0, d)
-            if dw.dtype != weight.dtype:
+            _probe_end(e0, d, "wgrad")
+            if dw is not None and dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         if ctx.has_res and ctx.needs_input_grad[3]:
             dres = g if ctx.res_scale == 1.0 else g * ctx.res_scale
             if dres.dtype != ctx.res_dtype:
                 dres = dres.to(ctx.res_dtype)
-        return dx, dw, dbias, dres, None, None, None, None
+        return dx, dw, dbias, dres, None, None, None, None, None
+
+
+def _fused_target(p):
+    """p.grad when p opted into in-place gradient accumulation (FlatParams sets
+    p._tpg_fused_grad): the HIP kernels then add into the flat fp32 gradient buffer
+    directly instead of returning a fresh gradient for autograd to add.  Valid for
+    .backward() use (the train step); torch.autograd.grad callers must not opt in."""
+    if p is None or not getattr(p, "_tpg_fused_grad", False):
+        return None
+    gr = p.grad
+    if gr is None or gr.dtype != torch.float32:
+        return None
+    return gr
 
 
 def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_ZERO, act=None, residual=None,
-           res_scale=1.0, transposed=False, output_padding=(0, 0)):
+           res_scale=1.0, transposed=False, output_padding=(0, 0), wparam=None):
     """Functional entry: act is an activation module (LeakyReLU / ReLU) or None."""
     code = act_code(act)
     if code is None:
         raise ValueError("activation %r cannot be fused" % (act,))
     kh, kw = weight.shape[2], weight.shape[3]
     geom = ConvGeom(kh, kw, stride, pad, pad_mode, transposed, output_padding)
-    return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale))
+    return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale), wparam)
 
 
 def linear(x, weight, bias=None, act=None, image_hw=None):
@@ -261,11 +308,11 @@ def linear(x, weight, bias=None, act=None, image_hw=None):
     if x.dim() == 4:
         b, c, h, w = x.shape
         w4 = weight.view(out_f, c, h, w)
-        y = conv2d(x, w4, bias, act=act)
+        y = conv2d(x, w4, bias, act=act, wparam=weight)
     else:
         b = x.shape[0]
         w4 = weight.view(out_f, in_f, 1, 1)
-        y = conv2d(x.reshape(b, in_f, 1, 1), w4, bias, act=act)
+        y = conv2d(x.reshape(b, in_f, 1, 1), w4, bias, act=act, wparam=weight)
     return y.reshape(b, out_f)
 
 

@@ -58,6 +58,7 @@ class FlatParams:
         v.copy_(p.data)
         p.data = v
         p.grad = self._view(self.grad, p, off, n)
+        p._tpg_fused_grad = True  # HIP weight/bias gradients add straight into self.grad
 
     def zero_grad(self):
         self.grad.zero_()
