@@ -74,8 +74,9 @@ typedef struct tpg_conv_desc {
   int32_t act;                    /* TPG_ACT_* applied after bias (+ residual) */
   float slope;                    /* LeakyReLU negative slope */
   float res_scale;                /* ResidualBlock scaling_factor (ModificationLayer.py:300) */
-  int32_t ksplit;                 /* 0 = automatic split-K, >=1 forces */
-  int32_t reserved;
+  int32_t ksplit;                 /* 0 = automatic; >= 1 forces the K split (bwd_filter: pixel splits) */
+  int32_t algo;                   /* 0 = automatic; bwd_filter: 1..5 = tile 256x128, 128x128, 128x64,
+                                     64x128, 64x64 (used with ksplit >= 1; autotuners set both) */
 } tpg_conv_desc;
 
 /* Workspace bytes needed by op (TPG_OP_*) for this descriptor. */

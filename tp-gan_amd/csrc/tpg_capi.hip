@@ -625,26 +625,26 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
     a.cbp = (int)rup(a.Cb, 8);
     const int64_t ncols = a.bflat ? (int64_t)a.ntaps * a.cbp : a.Cb;
     const int ngrid = a.bflat ? 1 : a.ntaps;
-    // Tile and pixel-split choice from a measured cost model (tools/bench_layers.py
-    // sweeps): a block costs (k-tiles + O) k-tile times, O = 23 with the atomic epilogue
-    // (8 without a split); blocks run in rounds of (CUs x blocks per CU); work per
-    // k-tile scales with the tile area, 64-wide tiles pay 15% for lower operand reuse.
-    static const int cand[5][3] = {{256, 128, 1}, {128, 128, 1}, {128, 64, 2}, {64, 128, 2}, {64, 64, 2}};
+    // Default tile / pixel-split choice (padded MACs, 64-wide tiles charged 15% for their
+    // lower operand reuse; about 2048 blocks).  Callers that autotune pass their choice in
+    // the descriptor: algo = tile index + 1 into cand[], ksplit = pixel splits.
+    static const int cand[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
     const int kp = d->dtype == TPG_BF16 ? 64 : 32;
     const int nkt = cdiv(a.npix, kp);
     int bm = 0, bn = 0, bks = 1;
-    double best = -1.0;
-    for (auto& c : cand) {
-      const int64_t tiles = (int64_t)cdiv(a.Ca, c[0]) * ((ncols + c[1] - 1) / c[1]) * ngrid;
-      const double area = (double)c[0] * c[1] / 32768.0 * ((c[0] == 64 || c[1] == 64) ? 1.15 : 1.0);
-      const int64_t slots = 256 * (int64_t)c[2];
-      for (int ks = 1; ks <= std::min(nkt, 256); ++ks) {
-        const int kpb = cdiv(nkt, ks);
-        if (ks > 1 && cdiv(nkt, kpb) != ks) continue;  // same per-block work as a smaller ks
-        const int64_t rounds = (tiles * ks + slots - 1) / slots;
-        const double t = (double)rounds * (kpb + (ks > 1 ? 23 : 8)) * area;
-        if (best < 0 || t < best * 0.999) { best = t; bm = c[0]; bn = c[1]; bks = ks; }
+    {
+      int64_t best = -1;
+      for (auto& c : cand) {
+        const int64_t cost = (int64_t)rup(a.Ca, c[0]) * rup(ncols, c[1]) * ngrid * ((c[0] == 64 || c[1] == 64) ? 115 : 100);
+        if (best < 0 || cost < best) { best = cost; bm = c[0]; bn = c[1]; }
       }
+      const int tiles = cdiv(a.Ca, bm) * (int)((ncols + bn - 1) / bn) * ngrid;
+      bks = std::max(1, cdiv(2048, tiles));
+      bks = std::min(bks, std::max(1, a.npix / (kp * 8)));
+    }
+    if (d->algo >= 1 && d->algo <= 5 && d->ksplit >= 1) {
+      bm = cand[d->algo - 1][0]; bn = cand[d->algo - 1][1];
+      bks = std::min(d->ksplit, nkt);
     }
     if (const char* f = getenv("TPG_WGRAD_FORCE")) {  // tuning hook: "bm,bn,ks"
       int fm = 0, fn = 0, fk = 0;
@@ -663,6 +663,13 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
     if (pb < (1ll << 31) && qb < (1ll << 31)) {
       a.p_bytes = (int)pb;
       a.q_bytes = (int)qb;
+      // division-free DMA addressing (see tpg_wgrad2.hip)
+      a.fastp = !comp && P.stride[2] == (int64_t)PW * P.stride[3] && P.stride[0] == (int64_t)PH * P.stride[2];
+      a.fastq = a.bflat && a.qst_h == 1 && a.qst_w == 1 && a.pad_mode == 0 && QH == PH && QW == PW &&
+                Q.stride[2] == (int64_t)QW * Q.stride[3] && Q.stride[0] == (int64_t)QH * Q.stride[2] &&
+                (int64_t)PH * PW > kp;
+      a.dpy = kp / a.PW;
+      a.dpx = kp % a.PW;
       return hip_check(launch_wgrad2(a, d->dtype, wgrad2_cfg(bm, bn), bm, bn, (hipStream_t)stream), "wgrad2");
     }
   }

@@ -100,6 +100,9 @@ struct WgradArgs {
   int8_t dy[TPG_MAX_TAPS], dx[TPG_MAX_TAPS], tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
   int p_bytes, q_bytes;       // buffer extents for the DMA kernel (out-of-range reads -> 0)
   int bflat, cbp;             // wgrad2 tap-flattened columns: b' = tap * cbp + b, cbp = rup(Cb, 8)
+  int fastp;                  // P dense NHWC: DMA offset = pixel * p_sw + c, no division
+  int fastq;                  // Q dense, same grid as P, unit stride, zero pad, image > one k-tile:
+  int dpy, dpx;               //   per-lane (py, px) advanced by (dpy, dpx) = divmod(KP, PW) per k-tile
 };
 typedef WgradArgs Wgrad2Args;
 

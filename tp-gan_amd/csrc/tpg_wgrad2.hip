@@ -107,14 +107,52 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
       ldy[j] = dy; ldx[j] = dx; lcb[j] = col;
     }
   }
+  // Fast address paths (the common case; the generic FastDiv path below is ~4x the VALU
+  // and, quarter-rate multiplies included, would outrun the MFMAs it feeds):
+  //   P dense  -> byte offset = (pixel * p_sw + c) * ES = scalar(p0) + pconst[j]
+  //   Q fast   -> (py, px) of each lane's pixel carried from k-tile to k-tile by
+  //               (dpy, dpx) with two conditional wraps; offset = scalar(p0) + qconst[j]
+  const bool fastp = p.fastp, fastq = p.fastq;
+  const int PH = p.PH, dpy = p.dpy, dpx = p.dpx;
+  int pconst[GA], qconst[GB], qpy[GB], qpx[GB], qrow[GB], prow[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int o = (wave * GA + j) * 1024 + lane * 16;
+    const int row = o / RBA, pc = (o % RBA) / 16;
+    const int lc = pc ^ w2_swz<BF, RBA>(row);
+    prow[j] = row;
+    pconst[j] = (int)((row * psw + a0 + lc * EPC) * ES);
+  }
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int o = (wave * GB + j) * 1024 + lane * 16;
+    const int row = o / RBB;
+    qrow[j] = row;
+    const int pix = pbeg + row;
+    const int n = dv_phpw.div(pix), rem = pix - n * PHPW;
+    qpy[j] = dv_pw.div(rem);
+    qpx[j] = rem - qpy[j] * PW;
+    qconst[j] = (int)(((row + ldy[j] * QW + ldx[j]) * qsw_ + lcb[j]) * ES);
+    if (lcb[j] >= (FLAT ? p.cbp : Cb)) qpy[j] = -(1 << 28);  // channel past the columns: never valid
+  }
+  int adv_kt = 0;  // k-tile the (qpy, qpx) state describes
   const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.P), 0, p.p_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Q), 0, p.q_bytes, 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
 
-  // DMA of k-tile kt into ring slot `slot`
+  // DMA of k-tile kt into ring slot `slot` (kt is non-decreasing, +0 or +1 per call)
   auto issue = [&](int kt, int slot) {
     char* st = lds + slot * STAGE;
     const int p0 = pbeg + kt * KP;
+    if (fastp) {
+      const int s0 = p0 * (int)psw * ES;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const unsigned off = (p0 + prow[j] < pend) ? (unsigned)(s0 + pconst[j]) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(st + (wave * GA + j) * 1024),
+                                                 16, off, 0, 0, 0);
+      }
+    } else {
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
       const int o = (wave * GA + j) * 1024 + lane * 16;  // byte offset in the A image
@@ -131,6 +169,27 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(st + (wave * GA + j) * 1024),
                                                16, off, 0, 0, 0);
+    }
+    }
+    if (fastq) {
+      const bool adv = kt > adv_kt;
+      adv_kt = kt;
+      const int s0 = p0 * (int)qsw_ * ES;
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        if (adv) {
+          int px = qpx[j] + dpx, py = qpy[j] + dpy;
+          if (px >= PW) { px -= PW; ++py; }
+          if (py >= PH) py -= PH;
+          qpx[j] = px; qpy[j] = py;
+        }
+        const bool ok = (p0 + qrow[j] < pend) && (unsigned)(qpy[j] + ldy[j]) < (unsigned)QH &&
+                        (unsigned)(qpx[j] + ldx[j]) < (unsigned)QW;
+        const unsigned off = ok ? (unsigned)(s0 + qconst[j]) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rQ, (__attribute__((address_space(3))) void*)(st + BYTES_A + (wave * GB + j) * 1024), 16, off, 0, 0, 0);
+      }
+      return;
     }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
@@ -165,44 +224,52 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     if constexpr (BF) {
+      // Fragments of substep ks+1 are read while substep ks's MFMAs run: one tr read is
+      // issued after each MFMA (R reads over M MFMAs), then one counted wait.  The reads
+      // are inline asm (hipcc's LDS-DMA alias tracking would put a vmcnt(0) in front of
+      // builtin LDS reads); each fragment's two halves are consumed only after the wait,
+      // and the ISA is checked to hold them in place (no copies before the wait).
+      constexpr int NS = KP / 32;
+      constexpr int R = 2 * (MREP + NREP), M = MREP * NREP;
       const int q = l16 >> 2, p4 = l16 & 3;
-#pragma unroll
-      for (int ks = 0; ks < KP / 32; ++ks) {
-        bf16x8 af[MREP], bfr[NREP];
-#pragma unroll
-        for (int m = 0; m < MREP; ++m) {
-          const int col = wm * WTM + m * 16 + 4 * p4;
-          s16x4 h[2];
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int row = ks * 32 + 8 * g + 4 * hh + q;
-            const char* ad = A + row * RBA + (((col >> 3) ^ w2_swz<BF, RBA>(row)) << 4) + (col & 7) * 2;
-            h[hh] = tr_read(ad);
-          }
-          af[m] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[0], h[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      auto addr = [&](int ks, int r) -> const char* {
+        if (r < 2 * MREP) {
+          const int col = wm * WTM + (r >> 1) * 16 + 4 * p4;
+          const int row = ks * 32 + 8 * g + 4 * (r & 1) + q;
+          return A + row * RBA + (((col >> 3) ^ w2_swz<BF, RBA>(row)) << 4) + (col & 7) * 2;
         }
+        const int rr = r - 2 * MREP;
+        const int col = wn * WTN + (rr >> 1) * 16 + 4 * p4;
+        const int row = ks * 32 + 8 * g + 4 * (rr & 1) + q;
+        return B + row * RBB + (((col >> 3) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 7) * 2;
+      };
+      s16x4 h[2][R];
 #pragma unroll
-        for (int n = 0; n < NREP; ++n) {
-          const int col = wn * WTN + n * 16 + 4 * p4;
-          s16x4 h[2];
+      for (int r = 0; r < R; ++r) h[0][r] = tr_read(addr(0, r));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int row = ks * 32 + 8 * g + 4 * hh + q;
-            const char* ad = B + row * RBB + (((col >> 3) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 7) * 2;
-            h[hh] = tr_read(ad);
+      for (int ks = 0; ks < NS; ++ks) {
+        const int cur = ks & 1;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const int m = i / NREP, n = i % NREP;
+          const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
+                                                                               0, 1, 2, 3, 4, 5, 6, 7));
+          const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * n],
+                                                                               h[cur][2 * MREP + 2 * n + 1],
+                                                                               0, 1, 2, 3, 4, 5, 6, 7));
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[m][n], 0, 0, 0);
+          if (ks + 1 < NS) {
+#pragma unroll
+            for (int r = i * R / M; r < (i + 1) * R / M; ++r) h[cur ^ 1][r] = tr_read(addr(ks + 1, r));
           }
-          bfr[n] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[0], h[1], 0, 1, 2, 3, 4, 5, 6, 7));
+          __builtin_amdgcn_sched_barrier(0);
         }
-        // the tr reads are inline asm (invisible to hipcc's LDS-DMA alias tracking, which
-        // would otherwise put a vmcnt(0) in front of them): wait for them by hand and keep
-        // the MFMAs below the wait (§5.4 rule 18)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int m = 0; m < MREP; ++m)
-#pragma unroll
-          for (int n = 0; n < NREP; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+        if (ks + 1 < NS) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else {
 #pragma unroll

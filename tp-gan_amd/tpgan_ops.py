@@ -15,8 +15,8 @@ import ctypes
 
 import torch
 
-from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, ConvDesc,
-                       TpgTensor, check, dtype_code, load, stream_ptr, tt)
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, TPG_BF16,
+                       ConvDesc, TpgTensor, check, dtype_code, load, stream_ptr, tt)
 
 _DTYPE = [torch.float32]
 
@@ -172,6 +172,70 @@ class ConvGeom:
         return d
 
 
+# Weight-gradient autotuning: the tile (desc.algo 1..5) and pixel split (desc.ksplit) of
+# tpg_conv2d_bwd_filter are chosen per shape on first use by timing every candidate into a
+# scratch gradient (HIP events, device synchronised around each trial, so only during
+# warm-up).  bf16 only; the cache can be saved / loaded as JSON for reproducible runs.
+AUTOTUNE = {"enabled": True, "cache": {}, "trials": 0}
+_WG_SPLITS = (1, 2, 4, 8, 16, 32, 64)
+
+
+def _desc_tuple(d):
+    return (d.n, d.in_c, d.in_h, d.in_w, d.out_c, d.out_h, d.out_w, d.kh, d.kw, d.stride_h, d.stride_w,
+            d.pad_t, d.pad_b, d.pad_l, d.pad_r, d.pad_mode, d.transposed, d.dtype)
+
+
+def save_tuning(path):
+    import json
+    with open(path, "w") as f:
+        json.dump([[list(k[1]), k[0], v] for k, v in AUTOTUNE["cache"].items()], f)
+
+
+def load_tuning(path):
+    import json
+    with open(path) as f:
+        for key, op, v in json.load(f):
+            AUTOTUNE["cache"][(op, tuple(key))] = tuple(v)
+
+
+def _tuned_wgrad(lib, d, x, g, dwv):
+    """(algo, ksplit) for this weight-gradient shape, tuning it on first use."""
+    key = ("wgrad", _desc_tuple(d))
+    hit = AUTOTUNE["cache"].get(key)
+    if hit is not None:
+        return hit
+    if not AUTOTUNE["enabled"] or d.dtype != TPG_BF16:
+        return (0, 0)
+    scratch = torch.empty_strided(dwv.shape, dwv.stride(), dtype=torch.float32, device=dwv.device)
+    npix = d.n * (d.in_h * d.in_w if d.transposed else d.out_h * d.out_w)
+    nkt = (npix + 63) // 64
+    best, best_ms = (0, 0), None
+    torch.cuda.synchronize()
+    for algo in range(1, 6):
+        for ks in _WG_SPLITS:
+            if ks > nkt:
+                break
+            d.algo, d.ksplit = algo, ks
+            ms = []
+            for rep in range(3):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(scratch), None, 0, stream_ptr()))
+                e1.record()
+                e1.synchronize()
+                if rep:
+                    ms.append(e0.elapsed_time(e1))
+            AUTOTUNE["trials"] += 1
+            t = min(ms)
+            if best_ms is None or t < best_ms:
+                best, best_ms = (algo, ks), t
+    d.algo, d.ksplit = 0, 0
+    torch.cuda.synchronize()
+    AUTOTUNE["cache"][key] = best
+    return best
+
+
 def _ws(lib, desc, op, device):
     nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
     if nb == 0:
@@ -265,9 +329,12 @@ class _ConvAct(torch.autograd.Function):
                     dw = dw.contiguous(memory_format=torch.channels_last)
                 dwv = dw
             FLOPS["wgrad"] += _conv_flops(d)
+            algo, ks = _tuned_wgrad(lib, d, x, g, dwv)
+            d.algo, d.ksplit = algo, ks
             e0 = _probe_begin(d, "wgrad")
             check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dwv), None, 0, stream_ptr()))
             _probe_end(e0, d, "wgrad")
+            d.algo, d.ksplit = 0, 0
             if dw is not None and dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         if ctx.has_res and ctx.needs_input_grad[3]:
