@@ -41,6 +41,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as hipGraph(s); off by default: on ROCm 7 the captured graph runs the "
+                         "local-pathway side-stream branches serially (54.6 vs 47.1 ms/step measured)")
+    ap.add_argument("--segmented", action="store_true", help="one hipGraph per step phase even at world 1")
+    ap.add_argument("--probe-steps", type=int, default=2)
     return ap.parse_args()
 
 
@@ -70,26 +75,36 @@ def main():
     def match(d, which):
         return which == "fwd" and d.in_c == 206 and d.out_c == 206 and d.kh == 5 and d.in_h == 128
 
-    for _ in range(args.warmup):
+    # warm-up (autotunes the weight-gradient tiles), one eager step counted for the
+    # algorithmic FLOPs, then the step is captured as hipGraph(s)
+    for _ in range(max(args.warmup - 1, 0)):
         trainer.step(batch)
     tpgan_ops.reset_flops()
-    trainer.step(batch)  # one counted step for the algorithmic FLOPs
+    trainer.step(batch)
     flops_step = sum(tpgan_ops.FLOPS.values())
     torch.cuda.synchronize()
+    graphed = args.graph
+    if graphed:
+        trainer.capture(batch, warmup=1, segmented=args.segmented or None)
+        trainer.step_graphed()
+        run = trainer.step_graphed
+    else:
+        def run():
+            return trainer.step(batch)
 
-    tpgan_ops.PROBE["match"] = match
-    tpgan_ops.PROBE["events"] = []
+    if not graphed:
+        tpgan_ops.PROBE["match"] = match
+        tpgan_ops.PROBE["events"] = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.step(batch)
+        run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    tpgan_ops.PROBE["match"] = None
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -97,8 +112,18 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     faces = world * B * args.steps / elapsed
 
+    # dominant-kernel probe: HIP events around each launch on its launch stream.  Graph
+    # nodes cannot be bracketed, so with graphs the probe runs eager steps right after the
+    # timed region (same kernel, same shapes); eager runs probe the timed steps themselves.
+    if graphed:
+        tpgan_ops.PROBE["match"] = match
+        tpgan_ops.PROBE["events"] = []
+    for _ in range(args.probe_steps if graphed else 0):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    tpgan_ops.PROBE["match"] = None
     evs = tpgan_ops.PROBE["events"]
-    k_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in evs) / max(len(evs), 1)
+    k_ms = sum(ev[0].elapsed_time(ev[1]) for ev in evs) / max(len(evs), 1)
     k_flops = evs[0][2] if evs else 0
     achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
 
@@ -130,12 +155,16 @@ def main():
         "data": "synthetic (U[-1,1] Multi-PIE-shaped batch resident in HBM; random-init weights)",
         "config": {"workload": "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, "
                                "128x128, bf16", "global_batch": B * world, "per_gpu_batch": B,
-                   "parallelism": "dp%d" % world},
+                   "parallelism": "dp%d" % world,
+                   "launch": "eager" if not graphed else ("hipGraph x3 (per phase)" if (world > 1 or args.segmented)
+                                                          else "hipGraph (whole step)")},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                     "kernel": "tpg igemm fwd, enhance_features_128 (206->206, 5x5, 128x128, bs%d, +residual, "
+                     "kernel": "tpg halo_kernel fwd, enhance_features_128 (206->206, 5x5, 128x128, bs%d, +residual, "
                                "LeakyReLU)" % B,
-                     "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4), "launches": len(evs)},
+                     "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4), "launches": len(evs),
+                     "timing": ("HIP events on the launch stream, eager probe steps after the timed graph replays"
+                                if graphed else "HIP events on the launch stream over the timed steps")},
         "step_mfma": {"algorithmic_tflop_per_step": round(flops_step / 1e12, 4),
                       "gflop_per_face": round(flops_step / B / 1e9, 2),
                       "achieved_tflops": round(flops_step / (ms_per_step * 1e-3) / 1e12, 2),

@@ -118,10 +118,13 @@ int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argm
                         tpg_stream_t stream);
 
 /* In-place Adam (torch.optim.Adam semantics, L2 weight_decay added to the gradient) on a
- * flat fp32 buffer; step is the 1-based step count after increment. grad_scale multiplies g. */
+ * flat fp32 buffer (all four pointers 16-byte aligned).  state is a caller-owned device
+ * float[4] {step, 1 - beta1^step, sqrt(1 - beta2^step), unused}, zero-initialised before the
+ * first call: step > 0 sets the step count explicitly, step == 0 advances the device counter
+ * by one (what a captured hipGraph replays).  grad_scale multiplies the gradient. */
 int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
-                 float grad_scale, tpg_stream_t stream);
+                 float grad_scale, float* state, tpg_stream_t stream);
 
 /* Library version string and the thread-local message of the last failed call. */
 const char* tpg_version(void);

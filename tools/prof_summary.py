@@ -1,43 +1,61 @@
-"""Summarise a rocprofv3 --kernel-trace --stats SQLite output (rocpd format) per kernel.
+"""Summarise a rocprofv3 --kernel-trace run (CSV kernel trace) per kernel over the timed steps.
 
-    python tools/prof_summary.py gpurun_out/prof5/run_results.db [--csv out.csv] [--steps N]
+    python tools/prof_summary.py gpurun_out/x/prof/run_kernel_trace.csv --steps 10 [--csv out.csv]
 
-Per-step figures divide by the number of train steps seen in the trace (Adam launches / 2,
-one per network per step) unless --steps is given.  Durations in the db are nanoseconds.
+The train step ends with one Adam launch per network (D then G), so the window of the last
+`--steps` steps starts right after the G Adam launch of the step before it; warm-up and
+weight-gradient autotuning trials fall outside the window.  Durations are nanoseconds.
 """
 import argparse
 import collections
 import csv
 import re
-import sqlite3
 
 
 def short(name):
     name = re.sub(r"\(tpg::\w+\)$", "", name)
-    name = name.replace("void tpg::", "")
+    name = name.replace("void tpg::", "").replace("tpg::", "")
     return name[:90]
+
+
+def load(path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    return rows
+
+
+def window(rows, steps):
+    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
+    if steps <= 0 or len(adam) < 2 * steps + 1:
+        return rows, max(1, len(adam) // 2)
+    first = adam[-(2 * steps + 1)] + 1
+    return rows[first:adam[-1] + 1], steps
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("db")
+    ap.add_argument("trace")
     ap.add_argument("--csv")
     ap.add_argument("--steps", type=int, default=0)
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
-    c = sqlite3.connect(a.db)
-    rows = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels").fetchall()
+    rows, steps = window(load(a.trace), a.steps)
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 1e30])
-    for name, dur, gx, gy, gz, wx in rows:
+    for t0, t1, name in rows:
+        dur = t1 - t0
         e = agg[short(name)]
         e[0] += 1
         e[1] += dur
         e[2] = max(e[2], dur)
         e[3] = min(e[3], dur)
-    steps = a.steps or max(1, agg.get("adam_kernel", [2])[0] // 2)
     total = sum(v[1] for v in agg.values())
+    span = (rows[-1][1] - rows[0][0]) if rows else 0
     items = sorted(agg.items(), key=lambda kv: -kv[1][1])
-    print("steps in trace: %d   total kernel time %.2f ms  (%.2f ms/step)" % (steps, total / 1e6, total / 1e6 / steps))
+    print("steps in window: %d   kernel time %.2f ms/step   wall span %.2f ms/step   (busy %.1f%%)" % (
+        steps, total / 1e6 / steps, span / 1e6 / steps, 100 * total / max(span, 1)))
     print("%-90s %7s %10s %9s %6s" % ("kernel", "calls", "ms/step", "avg_us", "%"))
     for k, (n, t, mx, mn) in items[:a.top]:
         print("%-90s %7d %10.3f %9.1f %6.2f" % (k, n, t / 1e6 / steps, t / n / 1e3, 100 * t / total))

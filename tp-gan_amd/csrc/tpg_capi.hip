@@ -31,7 +31,7 @@ extern "C" int32_t tpg_fuse_bwd_impl(int32_t, int32_t, int32_t, int32_t, tpg_ten
 extern "C" int32_t tpg_maxout_fwd_impl(int32_t, int32_t, tpg_tensor, tpg_tensor, uint8_t*, hipStream_t);
 extern "C" int32_t tpg_maxout_bwd_impl(int32_t, int32_t, tpg_tensor, const uint8_t*, tpg_tensor, hipStream_t);
 extern "C" int32_t tpg_adam_impl(int64_t, float*, const float*, float*, float*, float, float, float, float, float,
-                                  int32_t, float, hipStream_t);
+                                  int32_t, float, float*, hipStream_t);
 
 namespace tpg {
 int launch_reflect_fold(int N, int C, int H, int W, int pt, int pb, int pl, int pr, const tpg_tensor& dpad,
@@ -725,11 +725,14 @@ extern "C" int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const ui
 
 extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                             float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
-                            float grad_scale, tpg_stream_t stream) {
+                            float grad_scale, float* state, tpg_stream_t stream) {
   if (numel == 0) return 0;
-  return hip_check(tpg_adam_impl(numel, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step,
-                                 grad_scale, (hipStream_t)stream),
-                   "adam");
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !state) return fail(-10, "adam: NULL pointer");
+  if (step < 0) return fail(-2, "adam: step must be >= 0");
+  const int rc = tpg_adam_impl(numel, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step,
+                               grad_scale, state, (hipStream_t)stream);
+  if (rc == -1) return fail(-15, "adam: buffers must be 16-byte aligned");
+  return hip_check(rc, "adam");
 }
 
 extern "C" const char* tpg_version(void) { return "tpgan_hip 0.1 gfx950"; }

@@ -4,6 +4,7 @@
 // channels-last elements so that consecutive lanes touch consecutive channels.
 #include "tpg_internal.h"
 #include "../../include/tpgan.h"
+#include <stdlib.h>
 
 namespace tpg {
 
@@ -23,44 +24,53 @@ static inline int grid_for(int64_t total, int per_block = 256, int cap = 8192) {
 }
 
 // ------------------------------------------------------------------ weight packing --
-__global__ __launch_bounds__(256) void pack_kernel(const PackArgs p) {
-  const int64_t row_len = (int64_t)p.nunits * 16;
-  const int64_t total = (int64_t)p.Npad * row_len;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int np = (int)(idx / row_len);
-    const int kk = (int)(idx - (int64_t)np * row_len);
-    const int unit = kk >> 4;
-    const int tap = unit / p.upt;
-    const int cp = (unit - tap * p.upt) * 16 + (kk & 15);
-    float v = 0.f;
-    if (np < p.Nreal && tap < p.ntaps && cp < p.Creal) {
-      int a = 0, b = 0, r = p.tr[tap < TPG_MAX_TAPS ? tap : 0], s = p.ts[tap < TPG_MAX_TAPS ? tap : 0];
-      // decode n'
-      if (p.nmode == 0) a = np;
-      else if (p.nmode == 1) b = np;
-      else {
-        int rs = np / p.comp_c, ch = np - rs * p.comp_c;
-        r = rs / p.comp_kw; s = rs - r * p.comp_kw;
-        if (p.nmode == 2) b = ch; else a = ch;
-      }
-      // decode c'
-      if (p.cmode == 0) a = cp;
-      else if (p.cmode == 1) b = cp;
-      else {
-        int rs = cp / p.comp_c, ch = cp - rs * p.comp_c;
-        r = rs / p.comp_kw; s = rs - r * p.comp_kw;
-        if (p.cmode == 2) b = ch; else a = ch;
-      }
-      v = p.W[a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss];
-    }
-    st_any(p.Wp, p.dtype, idx, v);
+// One thread per 16-channel unit of one packed row, 32-bit index math.
+template <typename E>
+__global__ __launch_bounds__(256) void pack_kernel(const PackArgs p, int nthreads) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nthreads) return;
+  const int np = idx / p.nunits;
+  const int unit = idx - np * p.nunits;
+  const int tap = unit / p.upt;
+  const int cbase = (unit - tap * p.upt) * 16;
+  E out[16];
+  const bool ok = np < p.Nreal && tap < p.ntaps;
+  int a = 0, b = 0, r = ok ? p.tr[tap] : 0, s = ok ? p.ts[tap] : 0;
+  if (p.nmode == 0) a = np;
+  else if (p.nmode == 1) b = np;
+  else {
+    const int rs = np / p.comp_c, ch = np - rs * p.comp_c;
+    r = rs / p.comp_kw; s = rs - r * p.comp_kw;
+    if (p.nmode == 2) b = ch; else a = ch;
   }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int cp = cbase + e;
+    float v = 0.f;
+    if (ok && cp < p.Creal) {
+      int aa = a, bb = b, rr = r, ss = s;
+      if (p.cmode == 0) aa = cp;
+      else if (p.cmode == 1) bb = cp;
+      else {
+        const int rs = cp / p.comp_c, ch = cp - rs * p.comp_c;
+        rr = rs / p.comp_kw; ss = rs - rr * p.comp_kw;
+        if (p.cmode == 2) bb = ch; else aa = ch;
+      }
+      v = p.W[(int64_t)aa * p.w_sa + (int64_t)bb * p.w_sb + (int64_t)rr * p.w_sr + (int64_t)ss * p.w_ss];
+    }
+    out[e] = (E)v;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<E*>(p.Wp) + (int64_t)idx * 16);
+  const uint4* src = reinterpret_cast<const uint4*>(out);
+#pragma unroll
+  for (int q = 0; q < (int)(16 * sizeof(E) / 16); ++q) dst[q] = src[q];
 }
 
 int launch_pack(const PackArgs& a, hipStream_t s) {
-  int64_t total = (int64_t)a.Npad * a.nunits * 16;
-  hipLaunchKernelGGL(pack_kernel, dim3(grid_for(total)), dim3(256), 0, s, a);
+  const int nthreads = a.Npad * a.nunits;
+  const int blocks = (nthreads + 255) / 256;
+  if (a.dtype == TPG_BF16) hipLaunchKernelGGL(pack_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a, nthreads);
+  else hipLaunchKernelGGL(pack_kernel<float>, dim3(blocks), dim3(256), 0, s, a, nthreads);
   return (int)hipGetLastError();
 }
 
@@ -97,46 +107,69 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(int N, int C, int H, int W
 }
 
 // Vector form for channels-last tensors with pixel-dense, 16-byte aligned rows: a thread
-// owns one 16-byte channel chunk and walks pixels, so its dbias partials stay in registers;
-// block partials are combined in LDS, then one global atomic per channel per block.
+// owns one 16-byte channel chunk and walks a contiguous pixel range of its block, four
+// pixels per iteration with all loads issued before any use (HBM latency hiding).  Its
+// dbias partials stay in registers; the block combines them through LDS (no LDS atomics)
+// and adds one global atomic per channel, with at most 1024 blocks per launch.
 template <typename E>
 __global__ __launch_bounds__(256) void act_bwd_vec_kernel(int64_t npix, int C, int act, float slope, const E* gy,
                                                           int64_t gps, const E* y, int64_t yps, E* g, int64_t gps_out,
-                                                          float* dbias) {
+                                                          float* dbias, int64_t pix_per_block) {
   constexpr int EPC = 16 / sizeof(E);
-  __shared__ float sb[1024];
+  constexpr int U = 4;
+  __shared__ float sb[256 * EPC];
   const int nch = (C + EPC - 1) / EPC;
-  const int ppi = 256 / nch;                      // pixels per block iteration
+  const int ppi = 256 / nch;                      // pixel lanes per block
   const int ch = threadIdx.x % nch, pl = threadIdx.x / nch;
   const bool active = pl < ppi;
-  for (int i = threadIdx.x; i < nch * EPC; i += 256) sb[i] = 0.f;
-  __syncthreads();
   float part[EPC];
 #pragma unroll
   for (int e = 0; e < EPC; ++e) part[e] = 0.f;
   const int c0 = ch * EPC;
+  const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
+  const int64_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
+  const bool has_act = act != TPG_ACT_NONE;
   if (active) {
-    for (int64_t pix = (int64_t)blockIdx.x * ppi + pl; pix < npix; pix += (int64_t)gridDim.x * ppi) {
-      union { uint4 u; E e[EPC]; } vg, vy, vo;
-      vg.u = *reinterpret_cast<const uint4*>(gy + pix * gps + c0);
-      if (act != TPG_ACT_NONE) vy.u = *reinterpret_cast<const uint4*>(y + pix * yps + c0);
+    for (int64_t pb = p0 + pl; pb < p1; pb += (int64_t)U * ppi) {
+      union V { uint4 u; E e[EPC]; };
+      V vg[U], vy[U];
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) {
-        float v = (float)vg.e[e];
-        if (act != TPG_ACT_NONE && !((float)vy.e[e] > 0.f)) v = (act == TPG_ACT_LEAKY) ? v * slope : 0.f;
-        if (c0 + e >= C) v = 0.f;
-        vo.e[e] = (E)v;
-        part[e] += v;
+      for (int u = 0; u < U; ++u) {
+        const int64_t pix = pb + (int64_t)u * ppi;
+        if (pix < p1) {
+          vg[u].u = *reinterpret_cast<const uint4*>(gy + pix * gps + c0);
+          if (has_act) vy[u].u = *reinterpret_cast<const uint4*>(y + pix * yps + c0);
+        }
       }
-      *reinterpret_cast<uint4*>(g + pix * gps_out + c0) = vo.u;
-    }
 #pragma unroll
-    for (int e = 0; e < EPC; ++e)
-      if (c0 + e < C) atomicAdd(&sb[c0 + e], part[e]);
+      for (int u = 0; u < U; ++u) {
+        const int64_t pix = pb + (int64_t)u * ppi;
+        if (pix < p1) {
+          V vo;
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            float v = (float)vg[u].e[e];
+            if (has_act && !((float)vy[u].e[e] > 0.f)) v = (act == TPG_ACT_LEAKY) ? v * slope : 0.f;
+            if (c0 + e >= C) v = 0.f;
+            vo.e[e] = (E)v;
+            part[e] += v;
+          }
+          *reinterpret_cast<uint4*>(g + pix * gps_out + c0) = vo.u;
+        }
+      }
+    }
   }
+  if (!dbias) return;
+  // LDS layout [pixel lane][channel]: sb[pl * nch * EPC + c]
+#pragma unroll
+  for (int e = 0; e < EPC; ++e)
+    if (active) sb[pl * nch * EPC + c0 + e] = part[e];
   __syncthreads();
-  if (dbias)
-    for (int i = threadIdx.x; i < C; i += 256) atomicAdd(dbias + i, sb[i]);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int q = 0; q < ppi; ++q) s += sb[q * nch * EPC + c];
+    atomicAdd(dbias + c, s);
+  }
 }
 
 // ------------------------------------------------------------ strided 4-D copy --
@@ -281,20 +314,45 @@ int launch_reflect_fold(int N, int C, int H, int W, int pt, int pb, int pl, int 
 // ------------------------------------------------------------------------- Adam --
 // torch.optim.Adam (amsgrad=False, maximize=False): g += wd * p; m = b1 m + (1-b1) g;
 // v = b2 v + (1-b2) g^2; p -= lr / (1-b1^t) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
+// The bias corrections come from a device state {step, 1-b1^t, sqrt(1-b2^t)} that
+// adam_sched_kernel advances, so a captured hipGraph replays correct steps.
+__global__ void adam_sched_kernel(float* st, float b1, float b2, int32_t host_step) {
+  const float t = host_step > 0 ? (float)host_step : st[0] + 1.f;
+  st[0] = t;
+  st[1] = 1.f - powf(b1, t);
+  st[2] = sqrtf(1.f - powf(b2, t));
+}
+
+__device__ __forceinline__ void adam_one(float& pv, float g, float& mv, float& vv, float lr_bc1, float b1, float b2,
+                                         float eps, float wd, float bc2s) {
+  if (wd != 0.f) g += wd * pv;
+  mv = b1 * mv + (1.f - b1) * g;
+  vv = b2 * vv + (1.f - b2) * g * g;
+  pv = pv - lr_bc1 * mv / (sqrtf(vv) / bc2s + eps);
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ gr,
                                                    float* __restrict__ m, float* __restrict__ v, float lr, float b1,
-                                                   float b2, float eps, float wd, float bc1, float bc2s, float gscale) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float g = gr[i] * gscale;
-    float pv = p[i];
-    if (wd != 0.f) g += wd * pv;
-    float mv = b1 * m[i] + (1.f - b1) * g;
-    float vv = b2 * v[i] + (1.f - b2) * g * g;
-    m[i] = mv;
-    v[i] = vv;
-    float denom = sqrtf(vv) / bc2s + eps;
-    p[i] = pv - (lr / bc1) * mv / denom;
+                                                   float b2, float eps, float wd, const float* __restrict__ st,
+                                                   float gscale) {
+  const float lr_bc1 = lr / st[1], bc2s = st[2];
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 g = reinterpret_cast<const float4*>(gr)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_one(pv.x, g.x * gscale, mv.x, vv.x, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.y, g.y * gscale, mv.y, vv.y, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.z, g.z * gscale, mv.z, vv.z, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.w, g.w * gscale, mv.w, vv.w, lr_bc1, b1, b2, eps, wd, bc2s);
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(m)[i] = mv;
+    reinterpret_cast<float4*>(v)[i] = vv;
   }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    adam_one(p[i], gr[i] * gscale, m[i], v[i], lr_bc1, b1, b2, eps, wd, bc2s);
 }
 
 }  // namespace tpg
@@ -314,19 +372,22 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
                                      tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, hipStream_t s) {
   const int dt = g.dtype;
   const int epc = dt == TPG_BF16 ? 8 : 4;
-  if (c <= 1024 && (c + epc - 1) / epc <= 256 && pix_dense_vec(gy, h, w, dt, c) && pix_dense_vec(g, h, w, dt, c) &&
+  static const bool force_scalar = getenv("TPG_ACTB_SCALAR") != nullptr;  // debug switch
+  if (!force_scalar && c <= 1024 && (c + epc - 1) / epc <= 256 && pix_dense_vec(gy, h, w, dt, c) && pix_dense_vec(g, h, w, dt, c) &&
       (act == TPG_ACT_NONE || pix_dense_vec(y, h, w, dt, c))) {
     const int64_t npix = (int64_t)n * h * w;
     const int ppi = 256 / ((c + epc - 1) / epc);
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((npix + ppi - 1) / ppi, 2048));
+    // >= 16 pixels per lane, <= 1024 blocks (bounds the dbias atomics per channel)
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((npix + 16 * ppi - 1) / (16 * ppi), 1024));
+    const int64_t ppb = (npix + blocks - 1) / blocks;
     if (dt == TPG_BF16)
-      hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, npix, c, act, slope,
+      hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
                          (const __bf16*)gy.data, gy.stride[3], (const __bf16*)y.data, y.stride[3], (__bf16*)g.data,
-                         g.stride[3], dbias);
+                         g.stride[3], dbias, ppb);
     else
-      hipLaunchKernelGGL(act_bwd_vec_kernel<float>, dim3(blocks), dim3(256), 0, s, npix, c, act, slope,
+      hipLaunchKernelGGL(act_bwd_vec_kernel<float>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
                          (const float*)gy.data, gy.stride[3], (const float*)y.data, y.stride[3], (float*)g.data,
-                         g.stride[3], dbias);
+                         g.stride[3], dbias, ppb);
     return (int)hipGetLastError();
   }
   int64_t npix = (int64_t)n * h * w;
@@ -377,13 +438,17 @@ extern "C" int32_t tpg_maxout_bwd_impl(int32_t b, int32_t m, tpg_tensor gy, cons
   return (int)hipGetLastError();
 }
 
+// state: device float[4] {step, 1-b1^t, sqrt(1-b2^t), -}; host_step > 0 sets the step
+// explicitly, 0 advances the device counter (graph replay).
 extern "C" int32_t tpg_adam_impl(int64_t numel, float* param, const float* grad, float* m, float* v, float lr,
-                                  float b1, float b2, float eps, float wd, int32_t step, float gscale, hipStream_t s) {
-  float bc1 = 1.f - powf(b1, (float)step);
-  float bc2s = sqrtf(1.f - powf(b2, (float)step));
-  int blocks = (int)std::min<int64_t>((numel + 255) / 256, 8192);
+                                  float b1, float b2, float eps, float wd, int32_t host_step, float gscale,
+                                  float* state, hipStream_t s) {
+  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, state, b1, b2, host_step);
+  const bool vec = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
+  if (!vec) return -1;
+  int blocks = (int)std::min<int64_t>((numel / 4 + 255) / 256, 4096);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, bc1,
-                     bc2s, gscale);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, state,
+                     gscale);
   return (int)hipGetLastError();
 }

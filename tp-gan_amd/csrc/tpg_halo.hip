@@ -334,35 +334,36 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s) {
 // Wp[ks*ntaps + tap][ntile][BNL rows][4 chunks][EPC]: row r of N-tile nt is output
 // n' = nt*BN + r (zero when r >= BN or n' >= Nout); chunk' = chunk ^ hswz(r) holds
 // logical channels c = ks*KS + chunk*EPC + e of that tap.
-__global__ __launch_bounds__(256) void pack_halo_kernel(const PackArgs p, int nks, int bn, int bnl, int ntiles) {
-  const int epc = p.dtype == 1 ? 8 : 4;
-  const int row = 4 * epc;  // elements per 64-byte row
-  const int64_t total = (int64_t)nks * p.ntaps * ntiles * bnl * row;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t rr = idx / row;
-    const int inrow = (int)(idx - rr * row);
-    const int r = (int)(rr % bnl);
-    rr /= bnl;
-    const int nt = (int)(rr % ntiles);
-    rr /= ntiles;
-    const int tap = (int)(rr % p.ntaps);
-    const int ks = (int)(rr / p.ntaps);
-    const int pchunk = inrow / epc, e = inrow - pchunk * epc;
-    const int chunk = pchunk ^ hswz(r);
-    const int c = ks * row + chunk * epc + e;
-    const int np = nt * bn + r;
-    float v = 0.f;
-    if (r < bn && np < p.Nreal && c < p.Creal) {
-      int a = 0, b = 0;
-      const int tr = p.tr[tap], ts = p.ts[tap];
-      if (p.nmode == 0) a = np; else b = np;
-      if (p.cmode == 0) a = c; else b = c;
-      v = p.W[a * p.w_sa + b * p.w_sb + tr * p.w_sr + ts * p.w_ss];
-    }
-    if (p.dtype == 1) reinterpret_cast<__bf16*>(p.Wp)[idx] = (__bf16)v;
-    else reinterpret_cast<float*>(p.Wp)[idx] = v;
+// One thread per 16-byte chunk, 32-bit index math (the packed image is < 2^31 elements).
+template <typename E>
+__global__ __launch_bounds__(256) void pack_halo_kernel(const PackArgs p, int nks, int bn, int bnl, int ntiles,
+                                                        int nchunks) {
+  constexpr int EPC = 16 / sizeof(E);
+  constexpr int ROW = 4 * EPC;  // elements per 64-byte row
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nchunks) return;
+  const int pchunk = idx & 3;
+  int rr = idx >> 2;
+  const int r = rr % bnl;
+  rr /= bnl;
+  const int nt = rr % ntiles;
+  rr /= ntiles;
+  const int tap = rr % p.ntaps;
+  const int ks = rr / p.ntaps;
+  const int c0 = ks * ROW + (pchunk ^ hswz(r)) * EPC;
+  const int np = nt * bn + r;
+  union { uint4 u; E e[EPC]; } o;
+  const bool row_ok = r < bn && np < p.Nreal;
+  const int tr = p.tr[tap], ts = p.ts[tap];
+  const int64_t base = (int64_t)tr * p.w_sr + (int64_t)ts * p.w_ss +
+                       (p.nmode == 0 ? (int64_t)np * p.w_sa : (int64_t)np * p.w_sb);
+  const int64_t cstride = p.cmode == 0 ? p.w_sa : p.w_sb;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e;
+    o.e[e] = (E)((row_ok && c < p.Creal) ? p.W[base + (int64_t)c * cstride] : 0.f);
   }
+  reinterpret_cast<uint4*>(p.Wp)[idx] = o.u;
 }
 
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles) {
@@ -370,10 +371,12 @@ size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles) {
 }
 
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s) {
-  const int64_t total = (int64_t)nks * a.ntaps * ntiles * halo_bnl(bn) * (a.dtype == 1 ? 32 : 16);
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(pack_halo_kernel, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles);
+  const int nchunks = nks * a.ntaps * ntiles * halo_bnl(bn) * 4;
+  const int blocks = (nchunks + 255) / 256;
+  if (a.dtype == 1)
+    hipLaunchKernelGGL(pack_halo_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles, nchunks);
+  else
+    hipLaunchKernelGGL(pack_halo_kernel<float>, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles, nchunks);
   return (int)hipGetLastError();
 }
 

@@ -56,7 +56,7 @@ EXPORTS = {
                                          ctypes.c_void_p]),
     "tpg_adam": (ctypes.c_int32, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p] + [ctypes.c_float] * 5 + [ctypes.c_int32, ctypes.c_float,
-                                                                              ctypes.c_void_p]),
+                                                                              ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_version": (ctypes.c_char_p, []),
     "tpg_last_error": (ctypes.c_char_p, []),
 }

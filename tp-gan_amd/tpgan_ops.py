@@ -503,8 +503,9 @@ def maxout2(x):
     return _Maxout2.apply(x)
 
 
-def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
-    """In-place Adam on flat fp32 buffers (torch.optim.Adam semantics)."""
+def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, state, step=0, grad_scale=1.0):
+    """In-place Adam on flat fp32 buffers (torch.optim.Adam semantics).  `state` is a device
+    float32[4] {step, bias corrections}; step=0 advances its counter on the device (graph-safe)."""
     lib = load()
     check(lib.tpg_adam(param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
-                       lr, beta1, beta2, eps, weight_decay, step, grad_scale, stream_ptr()))
+                       lr, beta1, beta2, eps, weight_decay, int(step), grad_scale, state.data_ptr(), stream_ptr()))

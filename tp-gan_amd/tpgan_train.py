@@ -39,6 +39,7 @@ class FlatParams:
         self.grad = torch.zeros(total, dtype=torch.float32, device=device)
         self.exp_avg = torch.zeros_like(self.data)
         self.exp_avg_sq = torch.zeros_like(self.data)
+        self.adam_state = torch.zeros(4, dtype=torch.float32, device=device)  # {step, bias corrections}
         self.step = 0
         off = 0
         for p in self.params:
@@ -66,7 +67,7 @@ class FlatParams:
     def adam(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0):
         self.step += 1
         tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
-                            weight_decay, self.step, grad_scale)
+                            weight_decay, self.adam_state, 0, grad_scale)
 
 
 class GradSync:
@@ -105,8 +106,9 @@ class TPGANTrainer:
     """
 
     def __init__(self, G, D, lr=1e-4, betas=(0.5, 0.999), compute_dtype=torch.bfloat16, loss_weights=None,
-                 gradient_penalty=False, process_group=None, identity_fn=None):
+                 gradient_penalty=False, process_group=None, identity_fn=None, use_dropout=True):
         self.G, self.D = G, D
+        self.use_dropout = use_dropout  # FeaturePredict dropout (D_and_G_model.py:331-348)
         dev = next(G.parameters()).device
         self.fG = FlatParams(G, dev)
         self.fD = FlatParams(D, dev)
@@ -125,14 +127,19 @@ class TPGANTrainer:
     def _allreduce(self, flat):
         self.sync.allreduce(flat)
 
-    def step(self, b):
-        w = self.w
+    # The step is three device phases separated by the two data-parallel exchanges:
+    #   A: zero grads, G forward, D-step forward/backward           -> all-reduce D grads
+    #   B: D Adam, G-step D forward, G losses, G backward            -> all-reduce G grads
+    #   C: G Adam
+    # Eager mode runs them back to back; graph mode (capture()) records each phase as a
+    # hipGraph sharing one memory pool and replays them around the RCCL calls.
+    def _phase_a(self, b):
         G, D = self.G, self.D
         self.fG.zero_grad()
         self.fD.zero_grad()
         with tpgan_ops.compute_dtype(self.dtype):
-            outs = G(b["I128"], b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], True)
-            fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = outs
+            outs = G(b["I128"], b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], self.use_dropout)
+            fake = outs[0]
             B = fake.shape[0]
             # ---- D-step (critic on real and detached fake as one 2B batch)
             real = tpgan_ops.to_cl(b["frontal"], self.dtype)
@@ -140,7 +147,13 @@ class TPGANTrainer:
             d_real, d_fake = d_both[:B], d_both[B:]
             loss_D = d_fake.mean() - d_real.mean()
             loss_D.backward()
-            self._allreduce(self.fD)
+        self._st = {"outs": outs, "loss_D": loss_D.detach()}
+
+    def _phase_b(self, b):
+        w = self.w
+        D = self.D
+        fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = self._st.pop("outs")
+        with tpgan_ops.compute_dtype(self.dtype):
             self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
             # ---- G-step through the frozen, updated D
             set_requires_grad(D.parameters(), False)
@@ -163,9 +176,71 @@ class TPGANTrainer:
         if self.identity_fn is not None:
             loss_G = loss_G + w["weight_identity_preserving"] * self.identity_fn(f32, front)
         loss_G.backward()
-        self._allreduce(self.fG)
+        self._st["loss_G"] = loss_G.detach()
+
+    def _phase_c(self, b):
         self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
-        return {"loss_D": loss_D.detach(), "loss_G": loss_G.detach()}
+        return {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
+
+    def step(self, b):
+        """One eager G+D train step."""
+        self._phase_a(b)
+        self._allreduce(self.fD)
+        self._phase_b(b)
+        self._allreduce(self.fG)
+        return self._phase_c(b)
+
+    def capture(self, b, warmup=3, segmented=None):
+        """Record the train step as hipGraphs (torch.cuda.CUDAGraph over HIP streams): one
+        graph per phase sharing a memory pool (world > 1: the RCCL all-reduces run between
+        replays) or a single graph (world == 1).  `b` becomes the static input batch;
+        step_graphed() copies new data into it.  Warm-up steps (which also run the
+        weight-gradient autotuner, and train the model) run on a side stream first, as
+        capture requires."""
+        self._static = {k: v.clone() for k, v in b.items()}
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.step(self._static)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        if segmented is None:
+            segmented = self.world > 1
+        phases = (self._phase_a, self._phase_b, self._phase_c)
+        self._graphs = []
+        if not segmented:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for ph in phases:
+                    out = ph(self._static)
+            self._graphs.append(g)
+        else:
+            pool = None
+            for ph in phases:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    out = ph(self._static)
+                pool = g.pool()
+                self._graphs.append(g)
+        self._graph_out = out
+        torch.cuda.synchronize()
+
+    def step_graphed(self, b=None):
+        """One train step by graph replay (capture() first)."""
+        if b is not None and b is not self._static:
+            for k, v in b.items():
+                self._static[k].copy_(v, non_blocking=True)
+        if len(self._graphs) == 1:
+            self._graphs[0].replay()
+        else:
+            ga, gb, gc = self._graphs
+            ga.replay()
+            self._allreduce(self.fD)
+            gb.replay()
+            self._allreduce(self.fG)
+            gc.replay()
+        return self._graph_out
 
 
 def synthetic_batch(B, device, seed=0):
