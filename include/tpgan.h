@@ -21,6 +21,11 @@
  *   tpg_local_fuse_fwd/bwd  LocalFuser (D_and_G_model.py:132-159): zero-pad + max over 4 parts
  *   tpg_maxout2_fwd/bwd     fc2 maxout, MaxPool1d(2,2) (D_and_G_model.py:214,290)
  *   tpg_adam                the optimizer update (UtilityMethods.py:14-41 getOptimizer 'Adam')
+ *   tpg_dwconv2d_*          depthwise 3x3 conv of MobileNetV2's inverted residuals (MobileNetV2.py:105)
+ *   tpg_maxpool2d_*         ResNet stem MaxPool2d(3, 2, 1) (ResNet.py:33)
+ *   tpg_avgpool_*           AdaptiveAvgPool2d(1) (MobileNetV2.py:173, ResNet.py:45)
+ *   tpg_bn_fold             eval-mode BatchNorm2d folded into conv weights (MobileNetV2.py:100-112)
+ *   tpg_bn_train_fwd/bwd    training-mode BatchNorm2d (+ fused activation) with running statistics
  *
  * Conventions
  *   - Every tensor is described by tpg_tensor: a device pointer, a dtype and the element
@@ -50,7 +55,7 @@ extern "C" {
 typedef void* tpg_stream_t; /* hipStream_t */
 
 enum { TPG_F32 = 0, TPG_BF16 = 1 };
-enum { TPG_ACT_NONE = 0, TPG_ACT_RELU = 1, TPG_ACT_LEAKY = 2 };
+enum { TPG_ACT_NONE = 0, TPG_ACT_RELU = 1, TPG_ACT_LEAKY = 2, TPG_ACT_RELU6 = 3 };
 enum { TPG_PAD_ZERO = 0, TPG_PAD_REFLECT = 1 };
 enum { TPG_OP_FWD = 0, TPG_OP_BWD_DATA = 1, TPG_OP_BWD_FILTER = 2 };
 
@@ -125,6 +130,59 @@ int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argm
 int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  float grad_scale, float* state, tpg_stream_t stream);
+
+/* ---- identity-feature extractors (MobileNetV2.py, ResNet.py, FeatureExtract.py) ---- */
+
+/* Depthwise Conv2d (groups == in_c == out_c, MobileNetV2.py:105), kernels up to 3x3, zero
+ * padding: y = act(dwconv(x, w) + bias [+ res_scale * residual]).  w logical [C][1][kh][kw]
+ * fp32 (any strides); x / y / residual channels-last, 16-byte aligned rows of desc.dtype. */
+int32_t tpg_dwconv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, const float* bias,
+                         tpg_tensor residual, tpg_tensor y, tpg_stream_t stream);
+/* dx = input gradient of the depthwise conv for the masked output gradient g (overwrites dx). */
+int32_t tpg_dwconv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx,
+                              tpg_stream_t stream);
+/* dw += weight gradient (fp32 dw, logical [C][1][kh][kw]). */
+int32_t tpg_dwconv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw,
+                                tpg_stream_t stream);
+
+/* MaxPool2d(k, s, p) (ResNet.py:33): padding never wins; argmax (uint8, NHWC order of y) is the
+ * first window tap r*k+s attaining the maximum.  bwd overwrites dx (gather form, no atomics). */
+int32_t tpg_maxpool2d_fwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t k, int32_t s, int32_t p,
+                          int32_t oh, int32_t ow, tpg_tensor x, tpg_tensor y, uint8_t* argmax,
+                          tpg_stream_t stream);
+int32_t tpg_maxpool2d_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t k, int32_t s, int32_t p,
+                          int32_t oh, int32_t ow, tpg_tensor gy, const uint8_t* argmax, tpg_tensor dx,
+                          tpg_stream_t stream);
+
+/* AdaptiveAvgPool2d(1) (MobileNetV2.py:173, ResNet.py:45): y[n][c] = mean over h x w
+ * (y logical [n][c][1][1]); bwd: dx = gy / (h*w) broadcast (overwrites dx). */
+int32_t tpg_avgpool_fwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor x, tpg_tensor y,
+                        tpg_stream_t stream);
+int32_t tpg_avgpool_bwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor gy, tpg_tensor dx,
+                        tpg_stream_t stream);
+
+/* Eval-mode BatchNorm2d folded into the preceding conv (MobileNetV2.py:100-112):
+ * w_out = w * gamma / sqrt(var + eps) per output channel, b_out = (bias - mean) * that + beta
+ * (bias may be NULL).  w / w_out logical [cout][cin][kh][kw] fp32, any strides. */
+int32_t tpg_bn_fold(int32_t cout, int32_t cin, int32_t kh, int32_t kw, tpg_tensor w, const float* bias,
+                    const float* gamma, const float* beta, const float* mean, const float* var, float eps,
+                    tpg_tensor w_out, float* b_out, tpg_stream_t stream);
+
+/* Training-mode BatchNorm2d over N*H*W per channel (+ fused activation), pixel-dense channels-last
+ * x / y of one dtype: y = act((x - mean) / sqrt(var + eps) * gamma + beta) with batch mean and
+ * biased variance; save_mean / save_invstd (float[c]) are kept for the backward; running stats
+ * (may both be NULL) move by momentum using the unbiased variance, as nn.BatchNorm2d.
+ * ws: float[2c] scratch. */
+int32_t tpg_bn_train_fwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor x, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var, float momentum,
+                         float eps, int32_t act, float slope, tpg_tensor y, float* save_mean,
+                         float* save_invstd, float* ws, tpg_stream_t stream);
+/* Backward of the above from dy (gradient of the activation output) and the saved y, x:
+ * dx (may have data NULL) overwritten; dgamma / dbeta (may be NULL) accumulated (+=). */
+int32_t tpg_bn_train_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
+                         tpg_tensor dy, tpg_tensor y, tpg_tensor x, const float* gamma,
+                         const float* save_mean, const float* save_invstd, tpg_tensor dx, float* dgamma,
+                         float* dbeta, float* ws, tpg_stream_t stream);
 
 /* Library version string and the thread-local message of the last failed call. */
 const char* tpg_version(void);

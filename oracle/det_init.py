@@ -63,3 +63,32 @@ def det_input(name: str, shape, seed: int = 0) -> np.ndarray:
 def det_state_dict(named_shapes, prefix: str, seed: int = 0):
     """{key: ndarray} for an iterable of (key, shape) using name prefix + key."""
     return {k: det_param(prefix + k, s, seed) for k, s in named_shapes}
+
+
+def det_bn(name: str, c: int, seed: int = 0):
+    """Deterministic, well-conditioned BatchNorm2d state for `name` (a state_dict prefix):
+    weight 1 + 0.25u, bias 0.1u, running_mean 0.1u, running_var in [1, 1.5)."""
+    return {"weight": 1.0 + 0.25 * det_uniform(name + "weight", c, seed),
+            "bias": 0.1 * det_uniform(name + "bias", c, seed),
+            "running_mean": 0.1 * det_uniform(name + "running_mean", c, seed),
+            "running_var": 1.25 + 0.25 * det_uniform(name + "running_var", c, seed)}
+
+
+def det_module_state(module, prefix: str, seed: int = 0):
+    """state_dict of `module` (torch) with det_param weights and det_bn BatchNorm states,
+    as float64 numpy arrays keyed like module.state_dict() (num_batches_tracked = 0)."""
+    import torch.nn as nn
+    out = {}
+    bn_prefixes = {n + "." if n else "": m for n, m in module.named_modules()
+                   if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d))}
+    for k, v in module.state_dict().items():
+        pre, leaf = (k.rsplit(".", 1) + [""])[:2] if "." in k else ("", k)
+        pre = pre + "." if pre else ""
+        if pre in bn_prefixes:
+            if leaf == "num_batches_tracked":
+                out[k] = np.zeros((), dtype=np.int64)
+            else:
+                out[k] = det_bn(prefix + pre, v.shape[0], seed)[leaf]
+        else:
+            out[k] = det_param(prefix + k, v.shape, seed)
+    return out

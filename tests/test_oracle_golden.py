@@ -1,6 +1,9 @@
 """CPU: the oracle (oracle/tpgan_oracle.py) against the golden vectors produced by
 running the reference itself (tests/golden/make_golden.py).  This pins the oracle that
 the GPU parity tests and the CPU baseline rely on."""
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -8,6 +11,8 @@ import torch
 from _cases import case_arrays, golden, rel
 from oracle import tpgan_oracle as O
 from oracle.det_init import det_param, det_uniform
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 G_OUT = ["I128_fake", "encoder_predict", "fused_local_fake", "le_fake", "re_fake", "nose_fake", "mouth_fake",
          "fused_local_real"]
@@ -126,3 +131,45 @@ def test_oracle_maxout():
     np.testing.assert_array_equal(y.detach().numpy(), A["y"])
     y.backward(torch.from_numpy(A["gy"]))
     np.testing.assert_array_equal(x.grad.numpy(), A["dx"])
+
+
+# ---- identity-feature extractor oracle vs the reference's own MobileNetV2 run
+def _mnv2_params(train=False):
+    import torch
+    F = golden("features_golden.npz")
+    sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
+    import MobileNetV2 as MN  # product module: only for the state_dict key/shape listing
+    from oracle.det_init import det_module_state
+    m = MN.MobileNetV2()
+    assert list(m.state_dict().keys()) == [str(k) for k in F["keys"]]
+    st = det_module_state(m, "mnv2/")
+    return F, {k: torch.from_numpy(np.asarray(v)).double() if np.asarray(v).dtype != np.int64
+               else torch.from_numpy(np.asarray(v)) for k, v in st.items()}
+
+
+def test_oracle_mobilenet_v2_eval():
+    import torch
+    from oracle import features_oracle as FO
+    F, P = _mnv2_params()
+    x = torch.from_numpy(F["in:x128"]).double()
+    loc, cls, feats = FO.mobilenet_v2(P, x, training=False)
+    assert rel(loc, F["eval:loc"]) < 1e-6
+    assert rel(cls, F["eval:cls"]) < 1e-6
+    assert rel(feats[0], F["eval:f0"]) < 1e-6
+    assert rel(feats[1], F["eval:f1"]) < 1e-6
+    x = torch.from_numpy(F["in:x256"]).double()
+    loc, cls, feats = FO.mobilenet_v2(P, x, training=False)
+    assert rel(loc, F["eval256:loc"]) < 1e-6 and rel(cls, F["eval256:cls"]) < 1e-6
+
+
+def test_oracle_mobilenet_v2_train():
+    import torch
+    from oracle import features_oracle as FO
+    F, P = _mnv2_params()
+    x = torch.from_numpy(F["in:x128"]).double()
+    loc, cls, feats = FO.mobilenet_v2(P, x, training=True)
+    assert rel(loc, F["train:loc"]) < 1e-6
+    assert rel(feats[1], F["train:f1"]) < 1e-6
+    for k in F.files:
+        if k.startswith("train:state:"):
+            assert rel(P[k[len("train:state:"):]], F[k]) < 1e-9, k

@@ -121,6 +121,15 @@ def _generic_forward(seq, x):
             pad = m
             i += 1
             continue
+        if (isinstance(m, nn.Conv2d) and pad is None and i + 1 < len(mods) and
+                isinstance(mods[i + 1], nn.BatchNorm2d)):
+            # Conv2d -> BatchNorm2d [-> act]: BN folded (eval) or batch statistics (train)
+            act = None
+            if i + 2 < len(mods) and tpgan_ops.act_code(mods[i + 2]) is not None and mods[i + 2] is not None:
+                act = mods[i + 2]
+            x = tpgan_ops.conv_bn_act(x, m, mods[i + 1], act)
+            i += 3 if act is not None else 2
+            continue
         if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
             act = None
             if i + 1 < len(mods) and tpgan_ops.act_code(mods[i + 1]) is not None and mods[i + 1] is not None:
@@ -129,11 +138,16 @@ def _generic_forward(seq, x):
             x = _apply_conv(m, x, pad, act)
             pad = None
         elif isinstance(m, nn.Linear):
+            bn = None
+            if i + 1 < len(mods) and isinstance(mods[i + 1], nn.BatchNorm1d):
+                bn = mods[i + 1]
+                i += 1
             act = None
             if i + 1 < len(mods) and tpgan_ops.act_code(mods[i + 1]) is not None:
                 act = mods[i + 1]
                 i += 1
-            x = tpgan_ops.linear(x, m.weight, m.bias, act=act)
+            x = tpgan_ops.linear(x, m.weight, m.bias, act=act) if bn is None else \
+                tpgan_ops.linear_bn_act(x, m, bn, act)
         else:
             x = m(x)
         i += 1
@@ -256,5 +270,11 @@ class ResidualBlock(nn.Module):
         last = self.layers[-1]
         if tpgan_ops.act_code(self.activation) is not None and last._parts() is not None:
             return last(h, residual=short, res_scale=self.scaling_factor, post_act=self.activation)
+        lm = list(last._modules.values())
+        if (tpgan_ops.act_code(self.activation) is not None and len(lm) == 2 and isinstance(lm[0], nn.Conv2d) and
+                isinstance(lm[1], nn.BatchNorm2d) and not lm[1].training):
+            # conv -> eval BN, + shortcut, activation: one fused launch (BN folded)
+            return tpgan_ops.conv_bn_act(h, lm[0], lm[1], act=self.activation, residual=short,
+                                         res_scale=self.scaling_factor)
         out = last(h) + self.scaling_factor * short
         return self.activation(out) if self.activation is not None else out

@@ -52,6 +52,11 @@ static int32_t fail(int32_t code, const char* fmt, ...) {
   return code;
 }
 
+int tpg::record_error(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+
 static int32_t hip_check(int e, const char* what) {
   if (e == 0) return 0;
   return fail(e > 0 ? e : -100, "%s failed: %s", what, e > 0 ? hipGetErrorString((hipError_t)e) : "bad config");

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(int N, int C, int H, int W
       float v = ld_any(gy.data, gy.dtype, n * gy.stride[0] + c * gy.stride[1] + h * gy.stride[2] + w * gy.stride[3]);
       if (act != TPG_ACT_NONE) {
         float yv = ld_any(y.data, y.dtype, n * y.stride[0] + c * y.stride[1] + h * y.stride[2] + w * y.stride[3]);
-        if (!(yv > 0.f)) v = (act == TPG_ACT_LEAKY) ? v * slope : 0.f;
+        v = tpg_act_grad(v, yv, act, slope);
       }
       st_any(g.data, g.dtype, n * g.stride[0] + c * g.stride[1] + h * g.stride[2] + w * g.stride[3], v);
       sum += v;
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void act_bwd_vec_kernel(int64_t npix, int C, i
 #pragma unroll
           for (int e = 0; e < EPC; ++e) {
             float v = (float)vg[u].e[e];
-            if (has_act && !((float)vy[u].e[e] > 0.f)) v = (act == TPG_ACT_LEAKY) ? v * slope : 0.f;
+            if (has_act) v = tpg_act_grad(v, (float)vy[u].e[e], act, slope);
             if (c0 + e >= C) v = 0.f;
             vo.e[e] = (E)v;
             part[e] += v;

@@ -49,11 +49,7 @@ __device__ __forceinline__ u32x4 mask_chunk4(u32x4 v, int c0, int C) {
   return v;
 }
 
-__device__ __forceinline__ float h_act(float v, int act, float slope) {
-  if (act == 2) return v > 0.f ? v : v * slope;
-  if (act == 1) return v > 0.f ? v : 0.f;
-  return v;
-}
+__device__ __forceinline__ float h_act(float v, int act, float slope) { return tpg_act(v, act, slope); }
 
 __device__ __forceinline__ int h_refl(int i, int n) {
   i = i < 0 ? -i : i;

@@ -33,11 +33,7 @@ namespace tpg {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-__device__ __forceinline__ float act_apply(float v, int act, float slope) {
-  if (act == 2) return v > 0.f ? v : v * slope;
-  if (act == 1) return v > 0.f ? v : 0.f;
-  return v;
-}
+__device__ __forceinline__ float act_apply(float v, int act, float slope) { return tpg_act(v, act, slope); }
 
 template <typename E>
 __device__ __forceinline__ float ld_f(const E* p) { return (float)(*p); }

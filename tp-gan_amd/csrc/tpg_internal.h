@@ -9,6 +9,24 @@
 
 namespace tpg {
 
+// Activation codes of tpg_conv_desc.act (include/tpgan.h): 0 none, 1 ReLU,
+// 2 LeakyReLU(slope), 3 ReLU6 (MobileNetV2.py:104,107 / :150,169).
+__device__ __forceinline__ float tpg_act(float v, int act, float slope) {
+  if (act == 2) return v > 0.f ? v : v * slope;
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 3) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
+// d act / d pre-activation from the saved OUTPUT y (all four are monotone, so the sign
+// pattern of y identifies the linear piece; ReLU6 passes gradient only on 0 < y < 6).
+__device__ __forceinline__ float tpg_act_grad(float g, float y, int act, float slope) {
+  if (act == 2) return y > 0.f ? g : g * slope;
+  if (act == 1) return y > 0.f ? g : 0.f;
+  if (act == 3) return (y > 0.f && y < 6.f) ? g : 0.f;
+  return g;
+}
+
 // Fast unsigned division by a runtime constant for n, d < 2^31 (round-up method):
 // s = ceil(log2 d), mul = ceil(2^(31+s) / d) < 2^32, q = umulhi(n, mul) >> (s - 1).
 struct FastDiv {
@@ -169,6 +187,9 @@ struct HaloArgs {
   float slope;
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
+
+// sets the thread-local message returned by tpg_last_error() (tpg_capi.hip); returns code
+int record_error(int code, const char* msg);
 
 // launchers (return hipError_t as int); cfg selects the tile shape
 int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s);

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtpgan_hip.so")
 
 TPG_F32, TPG_BF16 = 0, 1
-ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3
 PAD_ZERO, PAD_REFLECT = 0, 1
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
 
@@ -57,6 +57,25 @@ EXPORTS = {
     "tpg_adam": (ctypes.c_int32, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p] + [ctypes.c_float] * 5 + [ctypes.c_int32, ctypes.c_float,
                                                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_dwconv2d_fwd": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, ctypes.c_void_p, TpgTensor,
+                                          TpgTensor, ctypes.c_void_p]),
+    "tpg_dwconv2d_bwd_data": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor,
+                                               ctypes.c_void_p]),
+    "tpg_dwconv2d_bwd_filter": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor,
+                                                 ctypes.c_void_p]),
+    "tpg_maxpool2d_fwd": (ctypes.c_int32, [ctypes.c_int32] * 9 + [TpgTensor, TpgTensor, ctypes.c_void_p,
+                                                                  ctypes.c_void_p]),
+    "tpg_maxpool2d_bwd": (ctypes.c_int32, [ctypes.c_int32] * 9 + [TpgTensor, ctypes.c_void_p, TpgTensor,
+                                                                  ctypes.c_void_p]),
+    "tpg_avgpool_fwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor, ctypes.c_void_p]),
+    "tpg_avgpool_bwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor, ctypes.c_void_p]),
+    "tpg_bn_fold": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor] + [ctypes.c_void_p] * 5 +
+                    [ctypes.c_float, TpgTensor, ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_bn_train_fwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor] + [ctypes.c_void_p] * 4 +
+                         [ctypes.c_float, ctypes.c_float, ctypes.c_int32, ctypes.c_float, TpgTensor] +
+                         [ctypes.c_void_p] * 4),
+    "tpg_bn_train_bwd": (ctypes.c_int32, [ctypes.c_int32] * 5 + [ctypes.c_float, TpgTensor, TpgTensor, TpgTensor] +
+                         [ctypes.c_void_p] * 3 + [TpgTensor] + [ctypes.c_void_p] * 4),
     "tpg_version": (ctypes.c_char_p, []),
     "tpg_last_error": (ctypes.c_char_p, []),
 }

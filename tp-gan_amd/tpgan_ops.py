@@ -15,7 +15,7 @@ import ctypes
 
 import torch
 
-from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, TPG_BF16,
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, TPG_BF16,
                        ConvDesc, TpgTensor, check, dtype_code, load, stream_ptr, tt)
 
 _DTYPE = [torch.float32]
@@ -131,6 +131,8 @@ def act_code(act):
         return ACT_NONE, 0.0
     if isinstance(act, torch.nn.LeakyReLU):
         return ACT_LEAKY, float(act.negative_slope)
+    if isinstance(act, torch.nn.ReLU6):
+        return ACT_RELU6, 0.0
     if isinstance(act, torch.nn.ReLU):
         return ACT_RELU, 0.0
     return None
@@ -509,3 +511,274 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_de
     lib = load()
     check(lib.tpg_adam(param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
                        lr, beta1, beta2, eps, weight_decay, int(step), grad_scale, state.data_ptr(), stream_ptr()))
+
+
+# ---------------------------------------------------------------------------------------
+# Identity-feature extractor ops (MobileNetV2.py, ResNet.py): depthwise conv, BatchNorm
+# (eval: folded into the conv; train: batch statistics), max / average pooling.
+# ---------------------------------------------------------------------------------------
+def _dw_desc(n, c, h, w, oh, ow, kh, kw, stride, pad, dtype, act, slope, res_scale):
+    d = ConvDesc()
+    d.n, d.in_c, d.in_h, d.in_w = n, c, h, w
+    d.out_c, d.out_h, d.out_w = c, oh, ow
+    d.kh, d.kw, d.stride_h, d.stride_w = kh, kw, stride[0], stride[1]
+    d.pad_t, d.pad_b, d.pad_l, d.pad_r = pad[0], pad[0], pad[1], pad[1]
+    d.dtype = dtype_code(dtype)
+    d.act, d.slope, d.res_scale = act, slope, res_scale
+    return d
+
+
+class _DWConv(torch.autograd.Function):
+    """Depthwise Conv2d (groups = C) + bias [+ residual] + activation (MobileNetV2.py:105-107)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, stride, pad, act, slope, res_scale):
+        lib = load()
+        dtype = get_compute_dtype()
+        x = to_cl(x, dtype)
+        n, c, h, w = x.shape
+        kh, kw = weight.shape[2], weight.shape[3]
+        if weight.shape[0] != c or weight.shape[1] != 1:
+            raise RuntimeError("depthwise weight %s does not match %d channels" % (tuple(weight.shape), c))
+        oh = (h + 2 * pad[0] - kh) // stride[0] + 1
+        ow = (w + 2 * pad[1] - kw) // stride[1] + 1
+        y = new_act(n, c, oh, ow, dtype, x.device)
+        res = to_cl(residual, dtype) if residual is not None else None
+        d = _dw_desc(n, c, h, w, oh, ow, kh, kw, stride, pad, dtype, act, slope, res_scale)
+        wv = weight if weight.dtype == torch.float32 else weight.float()
+        FLOPS["fwd"] += 2 * n * oh * ow * c * kh * kw
+        check(lib.tpg_dwconv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bias.data_ptr() if bias is not None else None,
+                                   tt(res), tt(y), stream_ptr()))
+        ctx.save_for_backward(x, wv, y)
+        ctx.d = d
+        ctx.has_bias, ctx.has_res = bias is not None, residual is not None
+        ctx.in_dtype = ctx.res_dtype = None
+        ctx.wdtype = weight.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        x, wv, y = ctx.saved_tensors
+        d = ctx.d
+        n, c, oh, ow = y.shape
+        g = new_act(n, c, oh, ow, y.dtype, y.device)
+        dbias = torch.zeros(c, dtype=torch.float32, device=y.device) \
+            if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        check(lib.tpg_act_bwd(n, c, oh, ow, d.act, d.slope, tt(to_cl(gy, y.dtype)), tt(y), tt(g),
+                              dbias.data_ptr() if dbias is not None else None, stream_ptr()))
+        dx = dw = dres = None
+        if ctx.needs_input_grad[0]:
+            dx = new_act(*x.shape, dtype=x.dtype, device=x.device)
+            FLOPS["dgrad"] += 2 * n * oh * ow * c * d.kh * d.kw
+            check(lib.tpg_dwconv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(dx), stream_ptr()))
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros(wv.shape, dtype=torch.float32, device=wv.device)
+            FLOPS["wgrad"] += 2 * n * oh * ow * c * d.kh * d.kw
+            check(lib.tpg_dwconv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), stream_ptr()))
+            if ctx.wdtype != torch.float32:
+                dw = dw.to(ctx.wdtype)
+        if ctx.has_res and ctx.needs_input_grad[3]:
+            dres = g if d.res_scale == 1.0 else g * d.res_scale
+        return dx, dw, dbias, dres, None, None, None, None, None
+
+
+def dwconv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0), act=None, residual=None, res_scale=1.0):
+    code = act_code(act)
+    if code is None:
+        raise ValueError("activation %r cannot be fused" % (act,))
+    return _DWConv.apply(x, weight, bias, residual, tuple(stride), tuple(pad), code[0], code[1], float(res_scale))
+
+
+def bn_fold(weight, bias, bn):
+    """Eval-mode BatchNorm2d folded into the preceding conv: (w * g / sqrt(v + eps),
+    (b - m) * g / sqrt(v + eps) + beta).  HIP kernel (tpg_bn_fold) when nothing needs a
+    gradient; differentiable aten form (parameter-sized, a few elements per channel)
+    when the conv weight or the BN affine parameters are trained in eval mode."""
+    gamma = bn.weight if bn.affine else torch.ones_like(bn.running_mean)
+    beta = bn.bias if bn.affine else torch.zeros_like(bn.running_mean)
+    needs = torch.is_grad_enabled() and (weight.requires_grad or gamma.requires_grad or beta.requires_grad or
+                                         (bias is not None and bias.requires_grad))
+    if needs:
+        sc = gamma / torch.sqrt(bn.running_var + bn.eps)
+        wf = weight * sc.view(-1, 1, 1, 1)
+        bf = ((bias if bias is not None else 0.0) - bn.running_mean) * sc + beta
+        return wf, bf
+    lib = load()
+    co, ci, kh, kw = weight.shape
+    wf = torch.empty_strided(weight.shape, weight.stride(), dtype=torch.float32, device=weight.device)
+    bf = torch.empty(co, dtype=torch.float32, device=weight.device)
+    wv = weight.detach() if weight.dtype == torch.float32 else weight.detach().float()
+    with torch.no_grad():
+        check(lib.tpg_bn_fold(co, ci, kh, kw, tt(wv), bias.data_ptr() if bias is not None else None,
+                              gamma.detach().float().data_ptr(), beta.detach().float().data_ptr(),
+                              bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(bn.eps), tt(wf),
+                              bf.data_ptr(), stream_ptr()))
+    return wf, bf
+
+
+def _pix_dense(t):
+    """t itself when its channels-last rows are pixel-dense with a 16-byte pixel stride
+    (what the batch-statistics kernels walk), else a packed copy."""
+    n, c, h, w = t.shape
+    ps = t.stride(3)
+    if (t.stride(1) == 1 and ps % 8 == 0 and ps >= _ceil8(c) and t.stride(2) == ps * w and
+            t.stride(0) == ps * w * h and t.data_ptr() % 16 == 0):
+        return t
+    out = new_act(n, c, h, w, t.dtype, t.device)
+    check(load().tpg_copy4d(n, c, h, w, tt(t), tt(out), stream_ptr()))
+    return out
+
+
+class _BNTrain(torch.autograd.Function):
+    """Training-mode BatchNorm2d + activation (batch statistics, running stats updated)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn, act, slope):
+        lib = load()
+        dtype = get_compute_dtype()
+        x = _pix_dense(to_cl(x, dtype))
+        n, c, h, w = x.shape
+        y = new_act(n, c, h, w, dtype, x.device)
+        mean = torch.empty(c, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        ws = torch.empty(2 * c, dtype=torch.float32, device=x.device)
+        rm = bn.running_mean if bn.track_running_stats else None
+        rv = bn.running_var if bn.track_running_stats else None
+        mom = 0.1 if bn.momentum is None else float(bn.momentum)
+        check(lib.tpg_bn_train_fwd(n, c, h, w, tt(x), gamma.detach().float().data_ptr(),
+                                   beta.detach().float().data_ptr(), rm.data_ptr() if rm is not None else None,
+                                   rv.data_ptr() if rv is not None else None, mom, float(bn.eps), act, slope, tt(y),
+                                   mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), stream_ptr()))
+        if bn.track_running_stats:
+            bn.num_batches_tracked.add_(1)
+        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.act, ctx.slope = act, slope
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        x, y, gamma, mean, invstd = ctx.saved_tensors
+        n, c, h, w = x.shape
+        gy = _pix_dense(to_cl(gy, y.dtype))
+        dx = new_act(n, c, h, w, x.dtype, x.device) if ctx.needs_input_grad[0] else None
+        dgamma = torch.zeros(c, dtype=torch.float32, device=x.device) if ctx.needs_input_grad[1] else None
+        dbeta = torch.zeros(c, dtype=torch.float32, device=x.device) if ctx.needs_input_grad[2] else None
+        ws = torch.empty(2 * c, dtype=torch.float32, device=x.device)
+        check(lib.tpg_bn_train_bwd(n, c, h, w, ctx.act, ctx.slope, tt(gy), tt(y), tt(x),
+                                   gamma.detach().float().data_ptr(), mean.data_ptr(), invstd.data_ptr(), tt(dx),
+                                   dgamma.data_ptr() if dgamma is not None else None,
+                                   dbeta.data_ptr() if dbeta is not None else None, ws.data_ptr(), stream_ptr()))
+        if dgamma is not None and gamma.dtype != torch.float32:
+            dgamma = dgamma.to(gamma.dtype)
+        return dx, dgamma, dbeta, None, None, None
+
+
+def batchnorm_train(x, bn, act=None):
+    code = act_code(act)
+    if code is None:
+        raise ValueError("activation %r cannot be fused" % (act,))
+    gamma = bn.weight if bn.affine else torch.ones_like(bn.running_mean)
+    beta = bn.bias if bn.affine else torch.zeros_like(bn.running_mean)
+    return _BNTrain.apply(x, gamma, beta, bn, code[0], code[1])
+
+
+def conv_bn_act(x, conv, bn, act=None, residual=None, res_scale=1.0):
+    """Conv2d (dense or depthwise) -> BatchNorm2d -> activation [+ residual before the
+    activation] as HIP calls: eval mode folds BN into the conv (one fused launch),
+    train mode runs the conv then the batch-statistics BN with the activation fused."""
+    dw = conv.groups != 1
+    if dw and conv.groups != conv.in_channels:
+        raise NotImplementedError("grouped convolution other than depthwise")
+    ph, pw = conv.padding
+    if bn is None or not bn.training:
+        if bn is not None:
+            w, b = bn_fold(conv.weight, conv.bias, bn)
+        else:
+            w, b = conv.weight, conv.bias
+        if dw:
+            return dwconv2d(x, w, b, conv.stride, (ph, pw), act=act, residual=residual, res_scale=res_scale)
+        return conv2d(x, w, b, stride=tuple(conv.stride), pad=(ph, ph, pw, pw), act=act, residual=residual,
+                      res_scale=res_scale)
+    if residual is not None:
+        raise NotImplementedError("residual inside a training-mode conv-BN block")
+    if dw:
+        h = dwconv2d(x, conv.weight, conv.bias, conv.stride, (ph, pw))
+    else:
+        h = conv2d(x, conv.weight, conv.bias, stride=tuple(conv.stride), pad=(ph, ph, pw, pw))
+    return batchnorm_train(h, bn, act)
+
+
+class _MaxPool2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        lib = load()
+        x = to_cl(x, get_compute_dtype())
+        n, c, h, w = x.shape
+        oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+        y = new_act(n, c, oh, ow, x.dtype, x.device)
+        amax = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        check(lib.tpg_maxpool2d_fwd(n, c, h, w, k, s, p, oh, ow, tt(x), tt(y), amax.data_ptr(), stream_ptr()))
+        ctx.save_for_backward(amax)
+        ctx.geo = (n, c, h, w, k, s, p, oh, ow)
+        ctx.dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        (amax,) = ctx.saved_tensors
+        n, c, h, w, k, s, p, oh, ow = ctx.geo
+        dx = new_act(n, c, h, w, ctx.dtype, gy.device)
+        check(lib.tpg_maxpool2d_bwd(n, c, h, w, k, s, p, oh, ow, tt(to_cl(gy, ctx.dtype)), amax.data_ptr(), tt(dx),
+                                    stream_ptr()))
+        return dx, None, None, None
+
+
+def maxpool2d(x, kernel_size, stride, padding):
+    return _MaxPool2d.apply(x, int(kernel_size), int(stride), int(padding))
+
+
+class _AvgPool(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1): [n, c, h, w] -> [n, c, 1, 1]."""
+
+    @staticmethod
+    def forward(ctx, x):
+        lib = load()
+        x = to_cl(x, get_compute_dtype())
+        n, c, h, w = x.shape
+        y = new_act(n, c, 1, 1, x.dtype, x.device)
+        check(lib.tpg_avgpool_fwd(n, c, h, w, tt(x), tt(y), stream_ptr()))
+        ctx.geo = (n, c, h, w)
+        ctx.dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load()
+        n, c, h, w = ctx.geo
+        dx = new_act(n, c, h, w, ctx.dtype, gy.device)
+        gy = to_cl(gy.reshape(n, c, 1, 1), ctx.dtype)
+        check(lib.tpg_avgpool_bwd(n, c, h, w, tt(gy), tt(dx), stream_ptr()))
+        return dx
+
+
+def global_avgpool(x):
+    return _AvgPool.apply(x)
+
+
+def linear_bn_act(x, lin, bn, act=None):
+    """Linear -> BatchNorm1d [-> act] (ModificationLayer.linear with use_batchnorm,
+    ModificationLayer.py:204-231) as a 1x1 conv on [B, in, 1, 1] with the BN folded (eval)
+    or as batch statistics over the batch (train)."""
+    b = x.shape[0]
+    out_f, in_f = lin.weight.shape
+    x4 = x.reshape(b, in_f, 1, 1)
+    w4 = lin.weight.view(out_f, in_f, 1, 1)
+    if not bn.training:
+        wf, bf = bn_fold(w4, lin.bias, bn)
+        y = conv2d(x4, wf, bf, act=act)
+    else:
+        y = batchnorm_train(conv2d(x4, w4, lin.bias), bn, act)
+    return y.reshape(b, out_f)
