@@ -115,6 +115,10 @@ def dtype_code(dt):
     raise TypeError("tpgan ops support float32 and bfloat16, got %s" % dt)
 
 
+def dtype_from_code(code):
+    return torch.bfloat16 if code == TPG_BF16 else torch.float32
+
+
 def tt(t):
     """TpgTensor for a torch tensor of rank <= 4 (logical NCHW; missing dims get stride 0)."""
     if t is None:

@@ -16,7 +16,7 @@ import ctypes
 import torch
 
 from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, TPG_BF16,
-                       ConvDesc, TpgTensor, check, dtype_code, load, stream_ptr, tt)
+                       ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load, stream_ptr, tt)
 
 _DTYPE = [torch.float32]
 
@@ -290,6 +290,8 @@ class _ConvAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        if torch.is_grad_enabled():  # create_graph=True (WGAN-GP): differentiable backward
+            return _conv_act_backward_graph(ctx, gy)
         lib = load()
         x, weight, y = ctx.saved_tensors
         d = ctx.d
@@ -344,6 +346,131 @@ class _ConvAct(torch.autograd.Function):
             if dres.dtype != ctx.res_dtype:
                 dres = dres.to(ctx.res_dtype)
         return dx, dw, dbias, dres, None, None, None, None, None
+
+
+# ---- double backward (WGAN-GP): the backward of _ConvAct written as
+# autograd Functions whose own backwards are the same three HIP ops, so
+# torch.autograd.grad(..., create_graph=True) followed by .backward() runs entirely on
+# the conv kernels:
+#   g  = act'(y) * gy                (linear in gy; the mask is piecewise constant)
+#   dx = dgrad(g, w)      d/dg: fwd(., w)      d/dw: wgrad(., g)
+#   dw = wgrad(x, g)      d/dx: dgrad(g, .)    d/dg: fwd(x, .)
+#   y' = fwd(x, w)        d/dx: dgrad(., w)    d/dw: wgrad(x, .)
+def _plain_desc(d):
+    e = ConvDesc()
+    ctypes.memmove(ctypes.byref(e), ctypes.byref(d), ctypes.sizeof(ConvDesc))
+    e.act, e.slope, e.res_scale, e.ksplit, e.algo = ACT_NONE, 0.0, 1.0, 0, 0
+    return e
+
+
+class _ActMask(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gy, y, act, slope):
+        lib = load()
+        n, c, h, w = y.shape
+        g = new_act(n, c, h, w, y.dtype, y.device)
+        check(lib.tpg_act_bwd(n, c, h, w, act, slope, tt(_fix_c1(to_cl(gy, y.dtype))), tt(y), tt(_fix_c1(g)), None,
+                              stream_ptr()))
+        ctx.save_for_backward(y)
+        ctx.act, ctx.slope = act, slope
+        return _fix_c1(g)
+
+    @staticmethod
+    def backward(ctx, dg):
+        (y,) = ctx.saved_tensors
+        return _ActMask.apply(dg, y, ctx.act, ctx.slope), None, None, None
+
+
+class _ConvFwdPlain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, d):
+        lib = load()
+        x = _fix_c1(to_cl(x, dtype_from_code(d.dtype)))
+        y = new_act(d.n, d.out_c, d.out_h, d.out_w, x.dtype, x.device)
+        ws = _ws(lib, d, OP_FWD, x.device)
+        FLOPS["fwd"] += _conv_flops(d)
+        check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w.float()), None, TpgTensor(), tt(_fix_c1(y)),
+                                 ws.data_ptr(), ws.numel(), stream_ptr()))
+        ctx.save_for_backward(x, w)
+        ctx.d = d
+        return _fix_c1(y)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = _ConvDgrad.apply(dy, w, ctx.d) if ctx.needs_input_grad[0] else None
+        dw = _ConvWgrad.apply(x, dy, ctx.d) if ctx.needs_input_grad[1] else None
+        return dx, dw, None
+
+
+class _ConvDgrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, w, d):
+        lib = load()
+        g = _fix_c1(to_cl(g, dtype_from_code(d.dtype)))
+        dx = new_act(d.n, d.in_c, d.in_h, d.in_w, g.dtype, g.device)
+        ws = _ws(lib, d, OP_BWD_DATA, g.device)
+        FLOPS["dgrad"] += _conv_flops(d)
+        check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w.float()), tt(_fix_c1(dx)), ws.data_ptr(),
+                                      ws.numel(), stream_ptr()))
+        ctx.save_for_backward(g, w)
+        ctx.d = d
+        return _fix_c1(dx)
+
+    @staticmethod
+    def backward(ctx, ddx):
+        g, w = ctx.saved_tensors
+        dg = _ConvFwdPlain.apply(ddx, w, ctx.d) if ctx.needs_input_grad[0] else None
+        dw = _ConvWgrad.apply(ddx, g, ctx.d) if ctx.needs_input_grad[1] else None
+        return dg, dw, None
+
+
+class _ConvWgrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, d):
+        lib = load()
+        dt = dtype_from_code(d.dtype)
+        x = _fix_c1(to_cl(x, dt))
+        g = _fix_c1(to_cl(g, dt))
+        if d.transposed:
+            shape = (d.in_c, d.out_c, d.kh, d.kw)
+        else:
+            shape = (d.out_c, d.in_c, d.kh, d.kw)
+        dw = torch.zeros(shape, dtype=torch.float32, device=x.device).contiguous(memory_format=torch.channels_last)
+        FLOPS["wgrad"] += _conv_flops(d)
+        check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0, stream_ptr()))
+        ctx.save_for_backward(x, g)
+        ctx.d = d
+        return dw
+
+    @staticmethod
+    def backward(ctx, ddw):
+        x, g = ctx.saved_tensors
+        dx = _ConvDgrad.apply(g, ddw, ctx.d) if ctx.needs_input_grad[0] else None
+        dg = _ConvFwdPlain.apply(x, ddw, ctx.d) if ctx.needs_input_grad[1] else None
+        return dx, dg, None
+
+
+def _conv_act_backward_graph(ctx, gy):
+    x, weight, y = ctx.saved_tensors
+    d = _plain_desc(ctx.d)
+    g = _ActMask.apply(gy, y, ctx.d.act, ctx.d.slope)
+    dx = dw = dbias = dres = None
+    if ctx.needs_input_grad[0]:
+        dx = _ConvDgrad.apply(g, weight, d)
+        if dx.dtype != ctx.in_dtype:
+            dx = dx.to(ctx.in_dtype)
+    if ctx.needs_input_grad[1]:
+        dw = _ConvWgrad.apply(x, g, d)
+        if tuple(dw.shape) != tuple(weight.shape):
+            dw = dw.reshape(weight.shape)
+    if ctx.has_bias and ctx.needs_input_grad[2]:
+        dbias = g.float().sum((0, 2, 3))
+    if ctx.has_res and ctx.needs_input_grad[3]:
+        dres = g if ctx.res_scale == 1.0 else g * ctx.res_scale
+        if dres.dtype != ctx.res_dtype:
+            dres = dres.to(ctx.res_dtype)
+    return dx, dw, dbias, dres, None, None, None, None, None
 
 
 def _fused_target(p):

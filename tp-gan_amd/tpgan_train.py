@@ -116,8 +116,6 @@ class TPGANTrainer:
         self.dtype = compute_dtype
         self.w = dict(LOSS_W if loss_weights is None else loss_weights)
         self.gp = gradient_penalty
-        if gradient_penalty:
-            raise NotImplementedError("WGAN-GP needs double backward through the HIP convs (next round)")
         self.sync = GradSync(process_group)
         self.world = self.sync.world
         self.identity_fn = identity_fn
@@ -146,8 +144,24 @@ class TPGANTrainer:
             d_both = D(torch.cat([real, fake.detach()], 0)).float()
             d_real, d_fake = d_both[:B], d_both[B:]
             loss_D = d_fake.mean() - d_real.mean()
+            if self.gp:
+                loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
             loss_D.backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
+
+    def gradient_penalty(self, real, fake, alpha=None):
+        """WGAN-GP (config.py:72 weight_gradient_penalty): mean over the batch of
+        (||grad_x D(x_hat)||_2 - 1)^2 at x_hat = a*real + (1-a)*fake, a ~ U[0,1) per sample.
+        The input gradient is taken with create_graph=True, so loss.backward() runs the
+        double backward through D on the HIP conv kernels (tpgan_ops._ConvDgrad/_ConvWgrad/
+        _ConvFwdPlain); parameter gradients of this first-order pass are not accumulated
+        into the flat buffer (tpgan_ops only fuses when no graph is being built)."""
+        B = real.shape[0]
+        a = torch.rand(B, 1, 1, 1, device=real.device, dtype=torch.float32) if alpha is None else alpha
+        x_hat = (a * real.float() + (1 - a) * fake.float()).requires_grad_(True)
+        d_hat = self.D(x_hat).float()
+        (gx,) = torch.autograd.grad(d_hat.sum(), x_hat, create_graph=True)
+        return ((gx.reshape(B, -1).float().norm(dim=1) - 1.0) ** 2).mean()
 
     def _phase_b(self, b):
         w = self.w
