@@ -46,6 +46,9 @@ def parse():
                          "local-pathway side-stream branches serially (54.6 vs 47.1 ms/step measured)")
     ap.add_argument("--segmented", action="store_true", help="one hipGraph per step phase even at world 1")
     ap.add_argument("--probe-steps", type=int, default=2)
+    ap.add_argument("--identity", choices=["none", "resnet50", "mobilenetv2"], default="none",
+                    help="identity-preserving loss extractor in the G step (BASELINE configs[2]: resnet50)")
+    ap.add_argument("--gp", action="store_true", help="WGAN-GP in the D step (double backward through D)")
     return ap.parse_args()
 
 
@@ -67,7 +70,13 @@ def main():
 
     G = DG.Generator(GCFG["zdim"], GCFG["num_classes"], use_batchnorm=False).to(dev)
     D = DG.Discriminator().to(dev)
-    trainer = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16)
+    identity_fn = None
+    if args.identity != "none":
+        import FeatureExtract as FE
+        ext = FE.FeatureExtractModel(args.identity, 347).to(dev)
+        identity_fn = FE.IdentityPreservingLoss(ext, torch.bfloat16)
+    trainer = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16, identity_fn=identity_fn,
+                                       gradient_penalty=args.gp)
     B = args.batch
     batch = tpgan_train.synthetic_batch(B, dev, seed=1000 + rank)
 
@@ -140,6 +149,23 @@ def main():
                "sample": "oracle/cpu_step.py full G+D train step (no optimizer), B=2, %d timed steps after 1 warm-up, "
                          "%.1f s/step, fp32 aten CPU" % (args.cpu_iters, dt)}
 
+    # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    # (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or null
+    traffic, traffic_src = None, None
+    pmc = os.path.join(REPO, "profiles", "pmc_dominant.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            pj = json.load(f)
+        traffic = int(pj["traffic_bytes"])
+        traffic_src = ("profiles/pmc_dominant.json: rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, median per "
+                       "dispatch of tools/bench_layers.py enhance_128 fwd; algorithmic %d B (x, residual in, y out, "
+                       "weights)" % int(pj.get("algorithmic_bytes", 0)))
+    workload = "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, 128x128, bf16"
+    if args.identity != "none":
+        workload = ("BASELINE configs[2]: configs[1] + %s identity-preserving loss (frozen extractor, eval BN) "
+                    "in the G step" % {"resnet50": "ResNet-50", "mobilenetv2": "MobileNetV2"}[args.identity])
+    if args.gp:
+        workload += " + WGAN-GP (double backward through D)"
     out = {
         "metric": "faces/sec (G+D train step) at 128x128 bs32, 1/2/4/8 MI355X; % MFMA roofline",
         "value": round(faces, 2),
@@ -153,13 +179,13 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (U[-1,1] Multi-PIE-shaped batch resident in HBM; random-init weights)",
-        "config": {"workload": "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, "
-                               "128x128, bf16", "global_batch": B * world, "per_gpu_batch": B,
+        "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B,
                    "parallelism": "dp%d" % world,
                    "launch": "eager" if not graphed else ("hipGraph x3 (per phase)" if (world > 1 or args.segmented)
                                                           else "hipGraph (whole step)")},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "tpg halo_kernel fwd, enhance_features_128 (206->206, 5x5, 128x128, bs%d, +residual, "
                                "LeakyReLU)" % B,
                      "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4), "launches": len(evs),
