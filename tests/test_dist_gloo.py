@@ -68,3 +68,65 @@ def test_dp_gloo_world2():
         assert ok_b, "broadcast rank %d" % rank
         assert ok_r, "allreduce rank %d" % rank
         assert ok_v
+
+
+def _worker_overlap(rank, world, port, q):
+    sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import D_and_G_model as DG
+        import tpgan_ops
+        import tpgan_train
+        torch.manual_seed(5)
+        D = DG.Discriminator()
+        flat = tpgan_train.FlatParams(D, torch.device("cpu"))
+        sync = tpgan_train.OverlappedGradSync(flat, bucket_mb=2.0)  # several buckets
+        names = [n for n, _ in D.named_parameters()]
+        before = {n: p.detach().clone() for n, p in D.named_parameters()}
+        results = []
+        for step in range(2):
+            flat.grad.zero_()
+            sync.begin()
+            params = list(D.parameters())
+            # ranks report gradients in different orders; one parameter never reports
+            order = list(range(len(params))) if rank == 0 else list(reversed(range(len(params))))
+            for i in order:
+                p = params[i]
+                p.grad.copy_(torch.full_like(p, float(rank + 1) * (i + 1)))
+                if i != 3:
+                    tpgan_ops.GRAD_READY_HOOK[0](p)
+            nb = len(sync.buckets)
+            sync.finish()
+            ok = all(torch.allclose(p.grad, torch.full_like(p, 3.0 * (i + 1))) for i, p in enumerate(D.parameters()))
+            results.append((ok, nb))
+        same_values = all(torch.equal(before[n], p.detach()) for n, p in zip(names, D.parameters()))
+        q.put((rank, results, list(sync.flat.offsets), same_values, tpgan_ops.GRAD_READY_HOOK[0] is None))
+    except Exception as e:  # report instead of leaving the parent waiting on the queue
+        q.put((rank, [(False, repr(e))], [], False, False))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_overlapped_bucket_sync_gloo_world2():
+    """OverlappedGradSync: buckets issued in index order whatever order the gradients
+    complete in (ranks differ on purpose), unreported parameters flushed by finish(), the
+    learned layout (rank 0's completion order) identical on both ranks and value-preserving."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlap, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)])
+    for p in procs:
+        p.join(60)
+    for rank, results, offsets, same, unhooked in res:
+        assert all(ok for ok, _ in results), (rank, results)
+        assert results[0][1] > 2
+        assert same and unhooked
+    assert res[0][2] == res[1][2]

@@ -309,6 +309,7 @@ class _ConvAct(torch.autograd.Function):
         _probe_end(e0, d, "actb")
         if fused_b:
             dbias = None  # accumulated straight into bias.grad
+            _grad_ready(ctx.bparam)
         g = _fix_c1(g)
         dx = dw = dres = None
         wv = weight if weight.dtype == torch.float32 else weight.float()
@@ -339,6 +340,8 @@ class _ConvAct(torch.autograd.Function):
             check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dwv), None, 0, stream_ptr()))
             _probe_end(e0, d, "wgrad")
             d.algo, d.ksplit = 0, 0
+            if dw is None:
+                _grad_ready(ctx.wparam)
             if dw is not None and dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         if ctx.has_res and ctx.needs_input_grad[3]:
@@ -471,6 +474,17 @@ def _conv_act_backward_graph(ctx, gy):
         if dres.dtype != ctx.res_dtype:
             dres = dres.to(ctx.res_dtype)
     return dx, dw, dbias, dres, None, None, None, None, None
+
+
+# Data-parallel overlap (tpgan_train.OverlappedGradSync): called once the last kernel that
+# accumulates a fused parameter gradient has been enqueued on the current stream.
+GRAD_READY_HOOK = [None]
+
+
+def _grad_ready(p):
+    h = GRAD_READY_HOOK[0]
+    if h is not None:
+        h(p)
 
 
 def _fused_target(p):

@@ -41,11 +41,35 @@ class FlatParams:
         self.exp_avg_sq = torch.zeros_like(self.data)
         self.adam_state = torch.zeros(4, dtype=torch.float32, device=device)  # {step, bias corrections}
         self.step = 0
+        self.offsets = []
         off = 0
         for p in self.params:
             n = p.numel()
+            self.offsets.append(off)
             self._bind(p, off, n)
             off += n
+
+    def relayout(self, order):
+        """Re-place the parameters in the flat buffers in `order` (a permutation of
+        parameter indices): values, gradients and Adam moments move with them and every
+        parameter / .grad view is re-bound."""
+        assert sorted(order) == list(range(len(self.params)))
+        bufs = [self.data, self.grad, self.exp_avg, self.exp_avg_sq]
+        new = [torch.empty_like(b) for b in bufs]
+        offsets = [0] * len(self.params)
+        off = 0
+        for i in order:
+            n = self.params[i].numel()
+            for b, nb in zip(bufs, new):
+                nb[off:off + n].copy_(b[self.offsets[i]:self.offsets[i] + n])
+            offsets[i] = off
+            off += n
+        self.data, self.grad, self.exp_avg, self.exp_avg_sq = new
+        self.offsets = offsets
+        for i, p in enumerate(self.params):
+            n = p.numel()
+            p.data = self._view(self.data, p, offsets[i], n)
+            p.grad = self._view(self.grad, p, offsets[i], n)
 
     def _view(self, buf, p, off, n):
         flat = buf[off:off + n]
@@ -93,6 +117,137 @@ class GradSync:
         return 1.0 / self.world
 
 
+class OverlappedGradSync(GradSync):
+    """Bucketed gradient all-reduce overlapped with the backward.
+
+    The flat gradient buffer is cut into parameter-aligned buckets of ~bucket_mb.  During
+    the backward every fused HIP weight/bias-gradient launch reports its parameter
+    (tpgan_ops.GRAD_READY_HOOK); when all parameters of a bucket are in, an event is
+    recorded on each producing stream and the bucket's RCCL all-reduce is issued on a
+    communication stream that waits on those events — while the backward of the
+    remaining layers keeps the compute streams busy.  Buckets are issued strictly in
+    index order (a bucket that completes early waits for its predecessors), so every rank
+    issues the same collective sequence regardless of timing.  finish() issues what is
+    left (parameters that reported nothing are complete once backward() has returned)
+    and makes the current stream wait for all of them.
+
+    After the first step the parameters are re-laid out in the order rank 0 observed
+    their gradients completing (broadcast, so all ranks agree), which turns "bucket k is
+    ready" into "the k-th stretch of the backward is done" — DDP's bucket rebuild."""
+
+    def __init__(self, flat, group=None, bucket_mb=32.0):
+        super(OverlappedGradSync, self).__init__(group)
+        self.flat = flat
+        self.bucket_bytes = int(bucket_mb * 2 ** 20)
+        self.active = False
+        self.order_learned = False
+        self._build()
+
+    def _build(self):
+        f = self.flat
+        self.index = {id(p): i for i, p in enumerate(f.params)}
+        self.buckets = []  # (offset, numel, [param indices])
+        cur, start, size = [], None, 0
+        # walk the buffer from its end (the last-laid-out parameters finish first)
+        for i in sorted(range(len(f.params)), key=lambda j: f.offsets[j], reverse=True):
+            off, n = f.offsets[i], f.params[i].numel()
+            if cur and (size + n) * 4 > self.bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += n
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {}
+        self.spans = []
+        for b, idxs in enumerate(self.buckets):
+            lo = min(f.offsets[i] for i in idxs)
+            hi = max(f.offsets[i] + f.params[i].numel() for i in idxs)
+            assert hi - lo == sum(f.params[i].numel() for i in idxs), "bucket must be contiguous"
+            self.spans.append((lo, hi - lo))
+            for i in idxs:
+                self.bucket_of[i] = b
+
+    def begin(self):
+        if self.world == 1:
+            return
+        self.active = True
+        self.pending = [len(idxs) for idxs in self.buckets]
+        self.seen = set()
+        self.next = 0
+        self.works = []
+        self.order = []
+        self.events = [[] for _ in self.buckets]
+        cuda = self.flat.grad.is_cuda
+        if cuda and not hasattr(self, "comm"):
+            self.comm = torch.cuda.Stream(device=self.flat.grad.device)
+        tpgan_ops.GRAD_READY_HOOK[0] = self._ready
+
+    def _ready(self, p):
+        i = self.index.get(id(p))
+        if i is None or i in self.seen:
+            return
+        self.seen.add(i)
+        self.order.append(i)
+        b = self.bucket_of[i]
+        if self.flat.grad.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            self.events[b].append(ev)
+        self.pending[b] -= 1
+        while self.next < len(self.buckets) and self.pending[self.next] == 0:
+            self._issue(self.next)
+            self.next += 1
+
+    def _issue(self, b, after_stream=None):
+        off, n = self.spans[b]
+        view = self.flat.grad[off:off + n]
+        if self.flat.grad.is_cuda:
+            with torch.cuda.stream(self.comm):
+                for ev in self.events[b]:
+                    self.comm.wait_event(ev)
+                if after_stream is not None:
+                    self.comm.wait_stream(after_stream)
+                self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+        else:
+            self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def finish(self):
+        if not self.active:
+            return
+        tpgan_ops.GRAD_READY_HOOK[0] = None
+        self.active = False
+        cur = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
+        while self.next < len(self.buckets):
+            self._issue(self.next, after_stream=cur)
+            self.next += 1
+        for w in self.works:
+            w.wait()
+        self.works = []
+        if not self.order_learned:
+            self._learn_order()
+
+    def _learn_order(self):
+        """Rank 0's completion order (unreported parameters after it, in reverse
+        registration order), broadcast and applied to the flat layout on every rank."""
+        f = self.flat
+        n = len(f.params)
+        seen = set(self.order)
+        order = list(self.order) + [i for i in reversed(range(n)) if i not in seen]
+        t = torch.tensor(order, dtype=torch.int64, device=f.grad.device)
+        dist.broadcast(t, 0, group=self.group)
+        # layout: the first-completed parameters at the END of the buffer, so that the
+        # reverse-order bucketing of _build() follows the completion order
+        f.relayout([int(i) for i in reversed(t.tolist())])
+        self.order_learned = True
+        self._build()
+
+    def allreduce(self, flat):
+        if self.active:  # already being reduced bucket by bucket
+            return self.finish()
+        return super(OverlappedGradSync, self).allreduce(flat)
+
+
 def total_variation(x):
     return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
 
@@ -106,7 +261,8 @@ class TPGANTrainer:
     """
 
     def __init__(self, G, D, lr=1e-4, betas=(0.5, 0.999), compute_dtype=torch.bfloat16, loss_weights=None,
-                 gradient_penalty=False, process_group=None, identity_fn=None, use_dropout=True):
+                 gradient_penalty=False, process_group=None, identity_fn=None, use_dropout=True, overlap=True,
+                 bucket_mb=32.0):
         self.G, self.D = G, D
         self.use_dropout = use_dropout  # FeaturePredict dropout (D_and_G_model.py:331-348)
         dev = next(G.parameters()).device
@@ -118,12 +274,18 @@ class TPGANTrainer:
         self.gp = gradient_penalty
         self.sync = GradSync(process_group)
         self.world = self.sync.world
+        # G's 551 MB of gradients are reduced bucket by bucket during the G backward
+        self.gsync = OverlappedGradSync(self.fG, process_group, bucket_mb) if (overlap and self.world > 1) else None
+        self._capturing = False
         self.identity_fn = identity_fn
         self.sync.broadcast(self.fG)
         self.sync.broadcast(self.fD)
 
     def _allreduce(self, flat):
-        self.sync.allreduce(flat)
+        if flat is self.fG and self.gsync is not None and self.gsync.active:
+            self.gsync.finish()
+        else:
+            self.sync.allreduce(flat)
 
     # The step is three device phases separated by the two data-parallel exchanges:
     #   A: zero grads, G forward, D-step forward/backward           -> all-reduce D grads
@@ -189,6 +351,8 @@ class TPGANTrainer:
                   w["weight_cross_entropy"] * l_ce)
         if self.identity_fn is not None:
             loss_G = loss_G + w["weight_identity_preserving"] * self.identity_fn(f32, front)
+        if self.gsync is not None and not self._capturing:
+            self.gsync.begin()
         loss_G.backward()
         self._st["loss_G"] = loss_G.detach()
 
@@ -221,6 +385,7 @@ class TPGANTrainer:
         torch.cuda.synchronize()
         if segmented is None:
             segmented = self.world > 1
+        self._capturing = True  # graph replays reduce G in one call between phases
         phases = (self._phase_a, self._phase_b, self._phase_c)
         self._graphs = []
         if not segmented:
