@@ -82,10 +82,31 @@ typedef struct tpg_conv_desc {
   int32_t ksplit;                 /* 0 = automatic; >= 1 forces the K split (bwd_filter: pixel splits) */
   int32_t algo;                   /* 0 = automatic; bwd_filter: 1..5 = tile 256x128, 128x128, 128x64,
                                      64x128, 64x64 (used with ksplit >= 1; autotuners set both) */
+  int32_t flags;                  /* TPG_FLAG_*: WPACKED = w.data is the image tpg_conv2d_pack_jobs /
+                                     tpg_pack_run produced for this descriptor and op */
 } tpg_conv_desc;
+
+enum { TPG_FLAG_WPACKED = 1 };
 
 /* Workspace bytes needed by op (TPG_OP_*) for this descriptor. */
 size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op);
+
+/* Pre-packed weights (fwd and bwd_data convert the fp32 master weight into the kernels'
+ * tile order on every call unless desc.flags has TPG_FLAG_WPACKED):
+ *   tpg_conv2d_packed_bytes  bytes of the packed image of (d, op), op = FWD or BWD_DATA
+ *   tpg_conv2d_pack_jobs     describe packing w into wp as <= max_jobs opaque jobs of
+ *                            tpg_pack_job_bytes() each, written to host memory `jobs`;
+ *                            returns the job count (negative on error)
+ *   tpg_pack_prepare         lay a host job array out for one launch; returns its block count
+ *   tpg_pack_run             run n prepared jobs (copied to device memory) in ONE launch
+ * The image assumes 16-byte aligned channels-last activations (and dense NHWC for the
+ * full-kernel GEMM forms); a call whose tensors need another plan returns -21. */
+size_t tpg_conv2d_packed_bytes(const tpg_conv_desc* d, int32_t op);
+size_t tpg_pack_job_bytes(void);
+int32_t tpg_conv2d_pack_jobs(const tpg_conv_desc* d, int32_t op, tpg_tensor w, void* wp, void* jobs,
+                             int32_t max_jobs);
+int64_t tpg_pack_prepare(void* jobs, int32_t n);
+int32_t tpg_pack_run(const void* jobs_dev, int32_t n, int64_t nblocks, tpg_stream_t stream);
 
 /* y = act(conv(x, w) + bias [+ res_scale * residual]).  residual.data may be NULL; bias may be NULL. */
 int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, const float* bias,

@@ -226,3 +226,37 @@ def test_train_step_with_gp_flat(gpu):
     end = base + tr.fD.grad.numel() * 4
     assert all(base <= p.grad.data_ptr() < end for p in D.parameters())
     assert float(tr.fD.grad.abs().sum()) > 0
+
+
+def test_prepacked_weights_match_inline_packing(gpu):
+    """After a train step the FlatParams-managed convs use pre-packed weight images
+    (tpg_pack_run after Adam); G / D outputs and input gradients match the per-call packing
+    path to within the run-to-run floor."""
+    import tpgan_ops
+    import tpgan_train
+    G, D = _models(gpu)
+    tr = tpgan_train.TPGANTrainer(G, D, compute_dtype=torch.bfloat16, use_dropout=False)
+    b = tpgan_train.synthetic_batch(2, gpu, seed=21)
+    tr.step(b)
+    torch.cuda.synchronize()
+    assert len(tr.fG.pack_entries) > 50 and tr.fG.pack_table is not None
+
+    def run():
+        x = b["I128"].clone().requires_grad_(True)
+        with tpgan_ops.compute_dtype(torch.bfloat16):
+            outs = G(x, b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], False)
+            d = D(outs[0])
+        (outs[0].float().sum() + d.float().sum()).backward()
+        torch.cuda.synchronize()
+        return outs[0].detach().float().clone(), d.detach().float().clone(), x.grad.clone()
+
+    a = run()
+    a2 = run()  # run-to-run floor: split-K fp32 atomics (stride-2 convs, fc1) are order-dependent
+    tpgan_ops.PACK["enabled"] = False
+    try:
+        c = run()
+    finally:
+        tpgan_ops.PACK["enabled"] = True
+    for i in range(3):
+        floor = rel(a2[i].cpu(), a[i].cpu())
+        assert rel(c[i].cpu(), a[i].cpu()) <= max(3 * floor, 1e-6), (i, rel(c[i].cpu(), a[i].cpu()), floor)

@@ -433,7 +433,7 @@ extern "C" size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op) {
 // run a list of problems: pack -> [zero split-K] -> igemm -> [finalize]
 static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, const tpg_tensor& W, const float* bias,
                          int bias_mod, const tpg_tensor& R, float res_scale, const tpg_tensor& Y, int act, float slope,
-                         char* ws, size_t ws_bytes, hipStream_t s) {
+                         char* ws, size_t ws_bytes, hipStream_t s, const char* packed = nullptr) {
   size_t need = probs_ws(v);
   if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
   const bool vA = vec_ok(A, dtype);
@@ -444,6 +444,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     const int64_t ext = (int64_t)(P.h.N - 1) * std::abs(A.stride[0]) + (int64_t)(P.h.A_H - 1) * std::abs(A.stride[2]) +
                         (int64_t)(P.h.A_W - 1) * std::abs(A.stride[3]) + P.h.C + 64;
     if (!vA || ext >= (1ll << 31)) {
+      if (packed) return fail(-21, "pre-packed weights assume the halo kernel; these tensors need the generic one");
       P.halo = false;
       P.wp_bytes = P.g_wp;
       P.sk_bytes = P.g_sk;
@@ -451,8 +452,11 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
   }
   size_t off = 0;
   std::vector<char*> wps;
-  for (Prob& P : v) { wps.push_back(ws + off); off += std::max(P.wp_bytes, P.g_wp); }
-  char* sk = ws + off;
+  for (Prob& P : v) {
+    wps.push_back((packed ? const_cast<char*>(packed) : ws) + off);
+    off += std::max(P.wp_bytes, P.g_wp);
+  }
+  char* sk = ws + (packed ? 0 : off);
   for (size_t i = 0; i < v.size(); ++i) {
     Prob& P = v[i];
     IgemmArgs& a = P.a;
@@ -462,7 +466,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     k.Wp = wps[i];
     if (P.halo) {
       HaloArgs& h = P.h;
-      if (h.ntaps > 0) {
+      if (h.ntaps > 0 && !packed) {
         int e = launch_pack_halo(k, h.nks, h.BN, h.ntiles, s);
         if (e) return hip_check(e, "pack_halo");
       }
@@ -491,7 +495,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
       }
       continue;
     }
-    if (a.nunits > 0) {
+    if (a.nunits > 0 && !packed) {
       int e = launch_pack(k, s);
       if (e) return hip_check(e, "pack");
     }
@@ -534,19 +538,93 @@ static int32_t check_tensor(const tpg_tensor& t, int dtype, const char* name) {
   return 0;
 }
 
+// ------------------------------------------------------------ pre-packed weights --
+// The packed image of (d, op) is the weight part of the op's workspace for the plan the
+// op picks on 16-byte aligned channels-last tensors: one region per problem, in plan order.
+static std::vector<Prob> pack_plan(const tpg_conv_desc* d, int32_t op) {
+  if (op == TPG_OP_FWD) return plan_fwd(d, fwd_composite(d, nullptr, nullptr));
+  return plan_bwd_data(d, bwd_data_composite(d, nullptr, nullptr));
+}
+
+extern "C" size_t tpg_conv2d_packed_bytes(const tpg_conv_desc* d, int32_t op) {
+  if (check_desc(d) || (op != TPG_OP_FWD && op != TPG_OP_BWD_DATA)) return 0;
+  size_t b = 0;
+  for (const Prob& P : pack_plan(d, op)) b += std::max(P.wp_bytes, P.g_wp);
+  return b;
+}
+
+extern "C" size_t tpg_pack_job_bytes(void) { return sizeof(PackJob); }
+
+extern "C" int32_t tpg_conv2d_pack_jobs(const tpg_conv_desc* d, int32_t op, tpg_tensor w, void* wp, void* jobs,
+                                        int32_t max_jobs) {
+  int32_t rc = check_desc(d);
+  if (rc) return rc;
+  if (op != TPG_OP_FWD && op != TPG_OP_BWD_DATA) return fail(-2, "pack: op must be fwd or bwd_data");
+  if (!w.data || w.dtype != TPG_F32 || !wp || !jobs) return fail(-10, "pack: NULL / non-fp32 weight");
+  std::vector<Prob> v = pack_plan(d, op);
+  PackJob* out = reinterpret_cast<PackJob*>(jobs);
+  int n = 0;
+  size_t off = 0;
+  for (Prob& P : v) {
+    const size_t region = std::max(P.wp_bytes, P.g_wp);
+    const bool has = P.halo ? P.h.ntaps > 0 : P.a.nunits > 0;
+    if (has) {
+      if (n >= max_jobs) return fail(-22, "pack: more than %d jobs", max_jobs);
+      PackJob& j = out[n++];
+      memset(&j, 0, sizeof(j));
+      j.k = P.pk;
+      j.k.W = reinterpret_cast<const float*>(w.data);
+      j.k.w_sa = w.stride[0]; j.k.w_sb = w.stride[1]; j.k.w_sr = w.stride[2]; j.k.w_ss = w.stride[3];
+      j.k.Wp = reinterpret_cast<char*>(wp) + off;
+      if (P.halo) {
+        j.kind = 1;
+        j.nks = P.h.nks; j.bn = P.h.BN; j.bnl = (P.h.BN + 127) / 128 * 128; j.ntiles = P.h.ntiles;
+        j.items = j.nks * j.k.ntaps * j.ntiles * j.bnl * 4;
+      } else {
+        j.kind = 0;
+        j.items = j.k.Npad * j.k.nunits;
+      }
+      j.nblocks = cdiv(j.items, 256);
+    }
+    off += region;
+  }
+  return n;
+}
+
+extern "C" int64_t tpg_pack_prepare(void* jobs, int32_t n) {
+  PackJob* j = reinterpret_cast<PackJob*>(jobs);
+  int64_t b = 0;
+  for (int i = 0; i < n; ++i) {
+    j[i].first_block = (int)b;
+    b += j[i].nblocks;
+  }
+  return b;
+}
+
+extern "C" int32_t tpg_pack_run(const void* jobs_dev, int32_t n, int64_t nblocks, tpg_stream_t stream) {
+  if (n <= 0) return 0;
+  if (!jobs_dev || nblocks <= 0 || nblocks >= (1ll << 31)) return fail(-2, "pack_run: bad batch");
+  return hip_check(launch_pack_many(reinterpret_cast<const PackJob*>(jobs_dev), n, (int)nblocks, (hipStream_t)stream),
+                   "pack_run");
+}
+
 extern "C" int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, const float* bias,
                                   tpg_tensor residual, tpg_tensor y, void* ws, size_t ws_bytes, tpg_stream_t stream) {
   int32_t rc = check_desc(d);
   if (rc) return rc;
   if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(y, d->dtype, "y"))) return rc;
-  if (!w.data || w.dtype != TPG_F32) return fail(-13, "weight must be fp32");
+  if (!w.data || (w.dtype != TPG_F32 && !(d->flags & TPG_FLAG_WPACKED))) return fail(-13, "weight must be fp32");
   if (residual.data && (rc = check_tensor(residual, d->dtype, "residual"))) return rc;
   const bool comp = fwd_composite(d, &x, &y);
+  const bool packed = d->flags & TPG_FLAG_WPACKED;
+  if (packed && comp != fwd_composite(d, nullptr, nullptr))
+    return fail(-21, "pre-packed weights assume a full-kernel GEMM; these tensors are not dense NHWC");
   std::vector<Prob> v = plan_fwd(d, comp);
   int bias_mod = (comp && d->transposed) ? d->out_c : 0;
   if (comp && residual.data) return fail(-14, "residual not supported on a full-kernel conv");
   return run_probs(v, d->dtype, x, w, bias, bias_mod, residual, d->res_scale, y, d->act, d->slope,
-                   reinterpret_cast<char*>(ws), ws_bytes, (hipStream_t)stream);
+                   reinterpret_cast<char*>(ws), ws_bytes, (hipStream_t)stream,
+                   packed ? reinterpret_cast<const char*>(w.data) : nullptr);
 }
 
 extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx, void* ws,
@@ -554,16 +632,20 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
   int32_t rc = check_desc(d);
   if (rc) return rc;
   if ((rc = check_tensor(g, d->dtype, "g")) || (rc = check_tensor(dx, d->dtype, "dx"))) return rc;
-  if (!w.data || w.dtype != TPG_F32) return fail(-13, "weight must be fp32");
+  const bool packed = d->flags & TPG_FLAG_WPACKED;
+  if (!w.data || (w.dtype != TPG_F32 && !packed)) return fail(-13, "weight must be fp32");
   hipStream_t s = (hipStream_t)stream;
   const bool comp = bwd_data_composite(d, &g, &dx);
+  if (packed && comp != bwd_data_composite(d, nullptr, nullptr))
+    return fail(-21, "pre-packed weights assume a full-kernel GEMM; these tensors are not dense NHWC");
+  const char* pk = packed ? reinterpret_cast<const char*>(w.data) : nullptr;
   std::vector<Prob> v = plan_bwd_data(d, comp);
   tpg_tensor none;
   memset(&none, 0, sizeof(none));
   const bool refl = !comp && !d->transposed && d->pad_mode == TPG_PAD_REFLECT;
   if (!refl)
     return run_probs(v, d->dtype, g, w, nullptr, 0, none, 0.f, dx, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws),
-                     ws_bytes, s);
+                     ws_bytes, s, pk);
   // reflect: gradient of the padded input into a dense NHWC temp, then fold onto dx
   const size_t tmpb = reflect_tmp_bytes(d);
   if (ws_bytes < tmpb) return fail(-20, "workspace too small");
@@ -573,7 +655,7 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
   tmp.data = ws; tmp.dtype = d->dtype;
   tmp.stride[0] = (int64_t)PH * PW * Cp; tmp.stride[1] = 1; tmp.stride[2] = (int64_t)PW * Cp; tmp.stride[3] = Cp;
   rc = run_probs(v, d->dtype, g, w, nullptr, 0, none, 0.f, tmp, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws) + tmpb,
-                 ws_bytes - tmpb, s);
+                 ws_bytes - tmpb, s, pk);
   if (rc) return rc;
   return hip_check(launch_reflect_fold(d->n, d->in_c, d->in_h, d->in_w, d->pad_t, d->pad_b, d->pad_l, d->pad_r, tmp, dx, s),
                    "reflect_fold");

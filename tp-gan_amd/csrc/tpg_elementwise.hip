@@ -28,42 +28,45 @@ static inline int grid_for(int64_t total, int per_block = 256, int cap = 8192) {
 template <typename E>
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs p, int nthreads) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= nthreads) return;
-  const int np = idx / p.nunits;
-  const int unit = idx - np * p.nunits;
-  const int tap = unit / p.upt;
-  const int cbase = (unit - tap * p.upt) * 16;
-  E out[16];
-  const bool ok = np < p.Nreal && tap < p.ntaps;
-  int a = 0, b = 0, r = ok ? p.tr[tap] : 0, s = ok ? p.ts[tap] : 0;
-  if (p.nmode == 0) a = np;
-  else if (p.nmode == 1) b = np;
-  else {
-    const int rs = np / p.comp_c, ch = np - rs * p.comp_c;
-    r = rs / p.comp_kw; s = rs - r * p.comp_kw;
-    if (p.nmode == 2) b = ch; else a = ch;
-  }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int cp = cbase + e;
-    float v = 0.f;
-    if (ok && cp < p.Creal) {
-      int aa = a, bb = b, rr = r, ss = s;
-      if (p.cmode == 0) aa = cp;
-      else if (p.cmode == 1) bb = cp;
-      else {
-        const int rs = cp / p.comp_c, ch = cp - rs * p.comp_c;
-        rr = rs / p.comp_kw; ss = rs - rr * p.comp_kw;
-        if (p.cmode == 2) bb = ch; else aa = ch;
-      }
-      v = p.W[(int64_t)aa * p.w_sa + (int64_t)bb * p.w_sb + (int64_t)rr * p.w_sr + (int64_t)ss * p.w_ss];
+  if (idx < nthreads) pack_igemm_item<E>(p, idx);
+}
+
+// Every weight pack of a network in one launch: block b finds its job (binary search over
+// first_block), stages the job in LDS and packs items (b - first_block)*256 + tid.
+__global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restrict__ jobs, int n) {
+  __shared__ PackJob job;
+  __shared__ int jsel;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n - 1;
+    const int b = blockIdx.x;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].first_block <= b) lo = mid; else hi = mid - 1;
     }
-    out[e] = (E)v;
+    jsel = lo;
   }
-  uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<E*>(p.Wp) + (int64_t)idx * 16);
-  const uint4* src = reinterpret_cast<const uint4*>(out);
-#pragma unroll
-  for (int q = 0; q < (int)(16 * sizeof(E) / 16); ++q) dst[q] = src[q];
+  __syncthreads();
+  {
+    const int* src = reinterpret_cast<const int*>(jobs + jsel);
+    int* dst = reinterpret_cast<int*>(&job);
+    for (int i = threadIdx.x; i < (int)(sizeof(PackJob) / 4); i += 256) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int idx = (blockIdx.x - job.first_block) * 256 + threadIdx.x;
+  if (idx >= job.items) return;
+  if (job.kind == 1) {
+    if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx);
+    else pack_halo_item<float>(job.k, job.bn, job.bnl, job.ntiles, idx);
+  } else {
+    if (job.k.dtype == TPG_BF16) pack_igemm_item<__bf16>(job.k, idx);
+    else pack_igemm_item<float>(job.k, idx);
+  }
+}
+
+int launch_pack_many(const PackJob* jobs_dev, int n, int nblocks, hipStream_t s) {
+  if (n <= 0 || nblocks <= 0) return 0;
+  hipLaunchKernelGGL(pack_many_kernel, dim3(nblocks), dim3(256), 0, s, jobs_dev, n);
+  return (int)hipGetLastError();
 }
 
 int launch_pack(const PackArgs& a, hipStream_t s) {

@@ -181,10 +181,18 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
       const int hp = hbase[m] + toff;
       af[m] = H[hp * 4 + (g ^ hswz(hp))];
     }
+    // all B fragments of the step are read up front into their own registers: reusing one
+    // register quad across n made hipcc wait (lgkmcnt(0)) before every B read, exposing
+    // the LDS latency 7 times per step on the 224-wide tile
+    u32x4 bf[NREP];
 #pragma unroll
     for (int n = 0; n < NREP; ++n) {
       const int r = wn * WTN + n * 16 + l16;
-      const u32x4 bv = Wl[r * 4 + (g ^ hswz(r))];
+      bf[n] = Wl[r * 4 + (g ^ hswz(r))];
+    }
+#pragma unroll
+    for (int n = 0; n < NREP; ++n) {
+      const u32x4 bv = bf[n];
 #pragma unroll
       for (int m = 0; m < MREP; ++m) {
         if constexpr (BF) {
@@ -199,6 +207,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
         }
       }
     }
+    // schedule: every fragment read first, then the MFMAs (counted lgkmcnt waits instead
+    // of one full wait per B fragment)
+    __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP * (BF ? 1 : 4), 0);
   };
 
   // Software pipeline over steps s = ks*ntaps + t, one barrier per step:
@@ -399,32 +411,8 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s) {
 template <typename E>
 __global__ __launch_bounds__(256) void pack_halo_kernel(const PackArgs p, int nks, int bn, int bnl, int ntiles,
                                                         int nchunks) {
-  constexpr int EPC = 16 / sizeof(E);
-  constexpr int ROW = 4 * EPC;  // elements per 64-byte row
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= nchunks) return;
-  const int pchunk = idx & 3;
-  int rr = idx >> 2;
-  const int r = rr % bnl;
-  rr /= bnl;
-  const int nt = rr % ntiles;
-  rr /= ntiles;
-  const int tap = rr % p.ntaps;
-  const int ks = rr / p.ntaps;
-  const int c0 = ks * ROW + (pchunk ^ hswz(r)) * EPC;
-  const int np = nt * bn + r;
-  union { uint4 u; E e[EPC]; } o;
-  const bool row_ok = r < bn && np < p.Nreal;
-  const int tr = p.tr[tap], ts = p.ts[tap];
-  const int64_t base = (int64_t)tr * p.w_sr + (int64_t)ts * p.w_ss +
-                       (p.nmode == 0 ? (int64_t)np * p.w_sa : (int64_t)np * p.w_sb);
-  const int64_t cstride = p.cmode == 0 ? p.w_sa : p.w_sb;
-#pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int c = c0 + e;
-    o.e[e] = (E)((row_ok && c < p.Creal) ? p.W[base + (int64_t)c * cstride] : 0.f);
-  }
-  reinterpret_cast<uint4*>(p.Wp)[idx] = o.u;
+  if (idx < nchunks) pack_halo_item<E>(p, bn, bnl, ntiles, idx);
 }
 
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles) {

@@ -139,6 +139,92 @@ struct PackArgs {
   int8_t tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
 };
 
+// Batched weight packing (tpg_pack_run): one job per packed problem.  Jobs start on
+// 256-item boundaries (`first_block`), so every block of the batch kernel packs for
+// exactly one job.
+struct PackJob {
+  PackArgs k;
+  int kind;                   // 0: implicit-GEMM layout (pack_kernel), 1: halo layout (pack_halo_kernel)
+  int nks, bn, bnl, ntiles;   // halo layout
+  int items;                  // igemm: Npad * nunits 16-element units; halo: 16-byte chunks
+  int first_block;            // set by tpg_pack_prepare
+  int nblocks;
+};
+
+__device__ __forceinline__ int pack_hswz(int row) { return ((row >> 2) & 1) << 1; }
+
+// igemm layout: item = (n', unit) -> 16 consecutive elements of Wp row n'
+template <typename E>
+__device__ __forceinline__ void pack_igemm_item(const PackArgs& p, int idx) {
+  const int np = idx / p.nunits;
+  const int unit = idx - np * p.nunits;
+  const int tap = unit / p.upt;
+  const int cbase = (unit - tap * p.upt) * 16;
+  E out[16];
+  const bool ok = np < p.Nreal && tap < p.ntaps;
+  int a = 0, b = 0, r = ok ? p.tr[tap] : 0, s = ok ? p.ts[tap] : 0;
+  if (p.nmode == 0) a = np;
+  else if (p.nmode == 1) b = np;
+  else {
+    const int rs = np / p.comp_c, ch = np - rs * p.comp_c;
+    r = rs / p.comp_kw; s = rs - r * p.comp_kw;
+    if (p.nmode == 2) b = ch; else a = ch;
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int cp = cbase + e;
+    float v = 0.f;
+    if (ok && cp < p.Creal) {
+      int aa = a, bb = b, rr = r, ss = s;
+      if (p.cmode == 0) aa = cp;
+      else if (p.cmode == 1) bb = cp;
+      else {
+        const int rs = cp / p.comp_c, ch = cp - rs * p.comp_c;
+        rr = rs / p.comp_kw; ss = rs - rr * p.comp_kw;
+        if (p.cmode == 2) bb = ch; else aa = ch;
+      }
+      v = p.W[(int64_t)aa * p.w_sa + (int64_t)bb * p.w_sb + (int64_t)rr * p.w_sr + (int64_t)ss * p.w_ss];
+    }
+    out[e] = (E)v;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<E*>(p.Wp) + (int64_t)idx * 16);
+  const uint4* src = reinterpret_cast<const uint4*>(out);
+#pragma unroll
+  for (int q = 0; q < (int)(16 * sizeof(E) / 16); ++q) dst[q] = src[q];
+}
+
+// halo layout: Wp[ks*ntaps + tap][ntile][bnl rows][4 chunks][EPC]; item = one 16-byte chunk;
+// row r of N-tile nt is n' = nt*bn + r, chunk' = chunk ^ hswz(r)
+template <typename E>
+__device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bnl, int ntiles, int idx) {
+  constexpr int EPC = 16 / sizeof(E);
+  constexpr int ROW = 4 * EPC;
+  const int pchunk = idx & 3;
+  int rr = idx >> 2;
+  const int r = rr % bnl;
+  rr /= bnl;
+  const int nt = rr % ntiles;
+  rr /= ntiles;
+  const int tap = rr % p.ntaps;
+  const int ks = rr / p.ntaps;
+  const int c0 = ks * ROW + (pchunk ^ pack_hswz(r)) * EPC;
+  const int np = nt * bn + r;
+  union { uint4 u; E e[EPC]; } o;
+  const bool row_ok = r < bn && np < p.Nreal;
+  const int tr = p.tr[tap], ts = p.ts[tap];
+  const int64_t base = (int64_t)tr * p.w_sr + (int64_t)ts * p.w_ss +
+                       (p.nmode == 0 ? (int64_t)np * p.w_sa : (int64_t)np * p.w_sb);
+  const int64_t cstride = p.cmode == 0 ? p.w_sa : p.w_sb;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e;
+    o.e[e] = (E)((row_ok && c < p.Creal) ? p.W[base + (int64_t)c * cstride] : 0.f);
+  }
+  reinterpret_cast<uint4*>(p.Wp)[idx] = o.u;
+}
+
+int launch_pack_many(const PackJob* jobs_dev, int n, int nblocks, hipStream_t s);
+
 struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [+ res])
   const float* ws;
   int nslices;                // number of partial slices (1 for atomically accumulated ws)

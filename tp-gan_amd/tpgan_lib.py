@@ -31,7 +31,10 @@ class ConvDesc(ctypes.Structure):
         "n", "in_c", "in_h", "in_w", "out_c", "out_h", "out_w", "kh", "kw", "stride_h", "stride_w",
         "pad_t", "pad_b", "pad_l", "pad_r", "pad_mode", "transposed", "dtype", "act")] + [
         ("slope", ctypes.c_float), ("res_scale", ctypes.c_float), ("ksplit", ctypes.c_int32),
-        ("algo", ctypes.c_int32)]
+        ("algo", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+FLAG_WPACKED = 1
 
 
 EXPORTS = {
@@ -76,6 +79,12 @@ EXPORTS = {
                          [ctypes.c_void_p] * 4),
     "tpg_bn_train_bwd": (ctypes.c_int32, [ctypes.c_int32] * 5 + [ctypes.c_float, TpgTensor, TpgTensor, TpgTensor] +
                          [ctypes.c_void_p] * 3 + [TpgTensor] + [ctypes.c_void_p] * 4),
+    "tpg_conv2d_packed_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvDesc), ctypes.c_int32]),
+    "tpg_pack_job_bytes": (ctypes.c_size_t, []),
+    "tpg_conv2d_pack_jobs": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), ctypes.c_int32, TpgTensor, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_int32]),
+    "tpg_pack_prepare": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int32]),
+    "tpg_pack_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p]),
     "tpg_version": (ctypes.c_char_p, []),
     "tpg_last_error": (ctypes.c_char_p, []),
 }

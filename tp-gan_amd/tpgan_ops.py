@@ -15,8 +15,8 @@ import ctypes
 
 import torch
 
-from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, OP_BWD_DATA, OP_FWD, PAD_REFLECT, PAD_ZERO, TPG_BF16,
-                       ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load, stream_ptr, tt)
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_WPACKED, OP_BWD_DATA, OP_FWD, PAD_REFLECT,
+                       PAD_ZERO, TPG_BF16, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load, stream_ptr, tt)
 
 _DTYPE = [torch.float32]
 
@@ -238,6 +238,100 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     return best
 
 
+# ---- pre-packed weights (FlatParams-managed parameters) --------------------------------
+# A conv's fp32 master weight is converted to the kernels' bf16 tile order once per weight
+# update instead of inside every fwd / dgrad call: each (parameter, op, shape) gets a
+# persistent packed image; FlatParams.adam() repacks every image of its network with ONE
+# batched launch (tpg_pack_run) right after the Adam launch.
+PACK = {"enabled": True}
+
+
+class _PackEntry:
+    __slots__ = ("buf", "jobs", "njobs", "dev", "nblocks", "epoch")
+
+
+def _pack_entry(flat, key, d, op, w):
+    lib = load()
+    e = flat.pack_entries.get(key)
+    if e is not None:
+        return e
+    nb = lib.tpg_conv2d_packed_bytes(ctypes.byref(d), op)
+    if nb == 0:
+        flat.pack_entries[key] = None
+        return None
+    jb = lib.tpg_pack_job_bytes()
+    e = _PackEntry()
+    e.buf = torch.empty(nb, dtype=torch.uint8, device=w.device)
+    host = ctypes.create_string_buffer(jb * 64)
+    n = lib.tpg_conv2d_pack_jobs(ctypes.byref(d), op, tt(w), e.buf.data_ptr(), host, 64)
+    if n < 0:
+        check(n)
+    e.jobs = host.raw[:jb * n]
+    e.njobs = n
+    single = ctypes.create_string_buffer(e.jobs, len(e.jobs))
+    e.nblocks = lib.tpg_pack_prepare(single, n)
+    e.dev = torch.frombuffer(bytearray(single.raw), dtype=torch.uint8).to(w.device)
+    e.epoch = -1
+    flat.pack_entries[key] = e
+    flat.pack_table = None  # the batched table must be rebuilt
+    return e
+
+
+def _packed_weight(param, d, op, w):
+    """The packed image of w for (d, op) if param is FlatParams-managed, packing it now if
+    it was not packed since the last update; None otherwise."""
+    flat = getattr(param, "_tpg_flat", None)
+    if flat is None or not PACK["enabled"] or d.dtype != TPG_BF16 or w.dtype != torch.float32:
+        return None
+    key = (op, _desc_tuple(d), w.data_ptr(), tuple(w.stride()))
+    e = _pack_entry(flat, key, d, op, w)
+    if e is None:
+        return None
+    if e.epoch != flat.epoch:
+        if e.njobs:
+            check(load().tpg_pack_run(e.dev.data_ptr(), e.njobs, e.nblocks, stream_ptr()))
+        e.epoch = flat.epoch
+    return e.buf
+
+
+def repack(flat):
+    """Re-pack every weight image of `flat` in one launch (after its parameters changed)."""
+    entries = [e for e in flat.pack_entries.values() if e is not None and e.njobs]
+    if not entries:
+        return
+    lib = load()
+    if flat.pack_table is None:
+        raw = b"".join(e.jobs for e in entries)
+        n = sum(e.njobs for e in entries)
+        host = ctypes.create_string_buffer(raw, len(raw))
+        nblocks = lib.tpg_pack_prepare(host, n)
+        flat.pack_table = (torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(flat.data.device), n, nblocks)
+    dev, n, nblocks = flat.pack_table
+    check(lib.tpg_pack_run(dev.data_ptr(), n, nblocks, stream_ptr()))
+    for e in entries:
+        e.epoch = flat.epoch
+
+
+def _packed_tt(buf):
+    t = TpgTensor()
+    t.data = buf.data_ptr()
+    t.dtype = TPG_BF16
+    return t
+
+
+def _run_maybe_packed(fn_packed, fn_plain, d, pk):
+    """Call with the packed image (desc flag set); fall back to packing inside the call
+    when the tensors need a different plan (-21)."""
+    if pk is not None:
+        d.flags = FLAG_WPACKED
+        rc = fn_packed()
+        d.flags = 0
+        if rc != -21:
+            check(rc)
+            return
+    check(fn_plain())
+
+
 def _ws(lib, desc, op, device):
     nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
     if nb == 0:
@@ -275,8 +369,13 @@ class _ConvAct(torch.autograd.Function):
         wv = weight if weight.dtype == torch.float32 else weight.float()
         FLOPS["fwd"] += _conv_flops(d)
         e0 = _probe_begin(d, "fwd")
-        check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bias.data_ptr() if bias is not None else None,
-                                 tt(res), tt(_fix_c1(y)), ws.data_ptr(), ws.numel(), stream_ptr()))
+        pk = _packed_weight(wparam if wparam is not None else weight, d, OP_FWD, wv)
+        bptr = bias.data_ptr() if bias is not None else None
+        _run_maybe_packed(
+            lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), _packed_tt(pk), bptr, tt(res), tt(_fix_c1(y)),
+                                       ws.data_ptr(), ws.numel(), stream_ptr()),
+            lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bptr, tt(res), tt(_fix_c1(y)),
+                                       ws.data_ptr(), ws.numel(), stream_ptr()), d, pk)
         _probe_end(e0, d, "fwd")
         ctx.save_for_backward(x, weight, y)
         ctx.geom, ctx.act, ctx.slope, ctx.res_scale = geom, act, slope, res_scale
@@ -318,8 +417,12 @@ class _ConvAct(torch.autograd.Function):
             ws = _ws(lib, d, OP_BWD_DATA, x.device)
             FLOPS["dgrad"] += _conv_flops(d)
             e0 = _probe_begin(d, "dgrad")
-            check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(_fix_c1(dx)), ws.data_ptr(), ws.numel(),
-                                          stream_ptr()))
+            pk = _packed_weight(ctx.wparam, d, OP_BWD_DATA, wv)
+            _run_maybe_packed(
+                lambda: lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), _packed_tt(pk), tt(_fix_c1(dx)), ws.data_ptr(),
+                                                ws.numel(), stream_ptr()),
+                lambda: lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(_fix_c1(dx)), ws.data_ptr(),
+                                                ws.numel(), stream_ptr()), d, pk)
             _probe_end(e0, d, "dgrad")
             if dx.dtype != ctx.in_dtype:
                 dx = dx.to(ctx.in_dtype)

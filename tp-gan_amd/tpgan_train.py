@@ -41,6 +41,9 @@ class FlatParams:
         self.exp_avg_sq = torch.zeros_like(self.data)
         self.adam_state = torch.zeros(4, dtype=torch.float32, device=device)  # {step, bias corrections}
         self.step = 0
+        self.epoch = 0            # bumped by every optimizer update (pre-packed weight images follow it)
+        self.pack_entries = {}    # tpgan_ops pre-packed weight images of this network's convs
+        self.pack_table = None
         self.offsets = []
         off = 0
         for p in self.params:
@@ -66,6 +69,8 @@ class FlatParams:
             off += n
         self.data, self.grad, self.exp_avg, self.exp_avg_sq = new
         self.offsets = offsets
+        self.pack_entries = {}  # weights moved: packed images are rebuilt on next use
+        self.pack_table = None
         for i, p in enumerate(self.params):
             n = p.numel()
             p.data = self._view(self.data, p, offsets[i], n)
@@ -84,6 +89,7 @@ class FlatParams:
         p.data = v
         p.grad = self._view(self.grad, p, off, n)
         p._tpg_fused_grad = True  # HIP weight/bias gradients add straight into self.grad
+        p._tpg_flat = self
 
     def zero_grad(self):
         self.grad.zero_()
@@ -92,6 +98,8 @@ class FlatParams:
         self.step += 1
         tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
                             weight_decay, self.adam_state, 0, grad_scale)
+        self.epoch += 1
+        tpgan_ops.repack(self)
 
 
 class GradSync:
