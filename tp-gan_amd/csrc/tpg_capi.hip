@@ -274,9 +274,12 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   // split over k-steps until the grid covers the chip (each split >= 4 pipeline steps)
   const int64_t base = (((int64_t)N * h.tiles_h * h.tiles_w + bimg - 1) / bimg) * h.ntiles;
   int ks = 1;
-  if (base < 256) {
-    const int kps_min = cdiv(4, a.ntaps);
-    ks = (int)std::min<int64_t>(cdiv(256, (int)base), std::max(1, h.nks / kps_min));
+  static const int split_below = getenv("TPG_SPLIT_BELOW") ? atoi(getenv("TPG_SPLIT_BELOW")) : 256;  // tuning
+  static const int split_to = getenv("TPG_SPLIT_TO") ? atoi(getenv("TPG_SPLIT_TO")) : 256;
+  static const int split_steps = getenv("TPG_SPLIT_STEPS") ? atoi(getenv("TPG_SPLIT_STEPS")) : 4;
+  if (base < split_below) {
+    const int kps_min = cdiv(split_steps, a.ntaps);
+    ks = (int)std::min<int64_t>(cdiv(split_to, (int)base), std::max(1, h.nks / kps_min));
   }
   h.kps = cdiv(h.nks, std::max(ks, 1));
   h.ksplit = cdiv(h.nks, h.kps);

@@ -58,7 +58,7 @@ __device__ __forceinline__ int h_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-template <bool BF, int HL, int BN, int WM, int WN, int TPB>
+template <bool BF, int HL, int BN, int WM, int WN>
 __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   using E = typename std::conditional<BF, __bf16, float>::type;
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const int hcap = p.hcap;
-  constexpr int RS = 3 * TPB;                          // weight ring slots (one tap slice each)
+  constexpr int RS = 3;                                // weight ring slots (one tap slice each)
   u32x4* halo = lds;                                   // [2][hcap][4]
   u32x4* wts = lds + 2 * hcap * 4;                     // [RS][BNL][4] ring
   int* s_toff = reinterpret_cast<int*>(wts + RS * BNL * 4);  // [TPG_MAX_TAPS]
@@ -224,77 +224,29 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   const int ntaps = p.ntaps;
   const int total = nks * ntaps;
   __syncthreads();  // tap table
-  if constexpr (TPB == 1) {
-    if (total > 0) {
-      load_halo(0);
-      issue_w(0, 0);
-      issue_w(min(1, total - 1), 1);
-      store_halo(0);
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      int ks = 0, t = 0, slot = 0;
-      int toff = s_toff[0];
-      for (int s = 0; s < total; ++s) {
-        const bool more_ks = ks + 1 < nks;
-        if (t == 0 && more_ks) load_halo(ks + 1);
-        const int slot2 = slot == 0 ? 2 : slot - 1;  // (s + 2) % 3
-        issue_w(min(s + 2, total - 1), slot2);
-        const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];  // read ahead of its use
-        compute(ks & 1, slot, toff);
-        toff = toff_next;
-        if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
-        if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        slot = slot == 2 ? 0 : slot + 1;
-        if (++t == ntaps) { t = 0; ++ks; }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
+  if (total > 0) {
+    load_halo(0);
+    issue_w(0, 0);
+    issue_w(min(1, total - 1), 1);
+    store_halo(0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    int ks = 0, t = 0, slot = 0;
+    int toff = s_toff[0];
+    for (int s = 0; s < total; ++s) {
+      const bool more_ks = ks + 1 < nks;
+      if (t == 0 && more_ks) load_halo(ks + 1);
+      const int slot2 = slot == 0 ? 2 : slot - 1;  // (s + 2) % 3
+      issue_w(min(s + 2, total - 1), slot2);
+      const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];  // read ahead of its use
+      compute(ks & 1, slot, toff);
+      toff = toff_next;
+      if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
+      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      slot = slot == 2 ? 0 : slot + 1;
+      if (++t == ntaps) { t = 0; ++ks; }
     }
-  } else {
-    // Two taps per barrier (ntaps >= 4, planner-checked): group G = steps 2G, 2G+1 (may
-    // straddle a k-step boundary).  Ring of 6 one-tap slots, slot = step % 6; at the start
-    // of group G the slices of group G+2 are issued, at its end vmcnt(2*GL) retires group
-    // G+1's.  The next k-step's halo is loaded into registers in the group where the
-    // current k-step starts and written to LDS at the end of the group before the one
-    // that first reads it (ntaps >= 4 keeps the buffer it overwrites two groups idle).
-    if (total > 0) {
-      load_halo(0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) issue_w(min(j, total - 1), j);
-      store_halo(0);
-      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      int ks = 0, t = 0;  // k-step / tap of step s0
-      int slot = 0;       // s0 % 6
-      for (int s0 = 0; s0 < total; s0 += 2) {
-        const bool has1 = s0 + 1 < total;
-        int ks1 = ks, t1 = t + 1;
-        if (t1 == ntaps) { t1 = 0; ++ks1; }
-        // the k-step starting in this group (if any) triggers the next halo load
-        const int kstart = t == 0 ? ks : ((has1 && t1 == 0) ? ks1 : -1);
-        if (kstart >= 0 && kstart + 1 < nks) load_halo(kstart + 1);
-        const int slotA = slot + 4 >= 6 ? slot - 2 : slot + 4;  // (s0 + 4) % 6
-        const int slotB = slot + 5 >= 6 ? slot - 1 : slot + 5;  // (s0 + 5) % 6
-        issue_w(min(s0 + 4, total - 1), slotA);
-        issue_w(min(s0 + 5, total - 1), slotB);
-        const int toff0 = s_toff[t];
-        const int toff1 = s_toff[t1];
-        compute(ks & 1, slot, toff0);
-        if (has1) compute(ks1 & 1, slot + 1, toff1);
-        // steps s0+2, s0+3: does a k-step start there?  Then its halo goes to LDS now.
-        int ks2 = ks1, t2 = t1 + 1;
-        if (t2 == ntaps) { t2 = 0; ++ks2; }
-        int ks3 = ks2, t3 = t2 + 1;
-        if (t3 == ntaps) { t3 = 0; ++ks3; }
-        if (s0 + 2 < total && t2 == 0) store_halo(ks2 & 1);
-        else if (s0 + 3 < total && t3 == 0) store_halo(ks3 & 1);
-        if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        ks = ks2;
-        t = t2;
-        slot = slot + 2 == 6 ? 0 : slot + 2;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
   }
 
   // ---- epilogue: fused bias / residual / activation store, or an fp32 partial slice
@@ -358,27 +310,18 @@ int halo_cfg(int hl, int bn) {
   return 5 * (hl - 3) + bi;
 }
 
-size_t halo_lds_bytes(int hcap, int bn, int tpb) {
-  return (size_t)(2 * hcap * 4 + 3 * tpb * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
+// Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
+// 7x7 layers alone, -2 % on the train step) and a cross-barrier fragment prefetch with a
+// 4-slot ring (-2..12 %: the second fragment set pushed the 224-wide tile past 256 VGPRs).
+size_t halo_lds_bytes(int hcap, int bn) {
+  return (size_t)(2 * hcap * 4 + 3 * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
 }
 
-// two taps per barrier when the k-step has >= 4 taps and the 6-slot ring fits in LDS
-static int halo_tpb(const HaloArgs& a) {
-  static const int force = getenv("TPG_HALO_TPB") ? atoi(getenv("TPG_HALO_TPB")) : 0;  // tuning hook
-  if (force == 1) return 1;
-  // only when it costs no occupancy: 2 blocks/CU (80 KB each) beat fewer barriers
-  // (conv5_0 206->64 5x5: 0.46 ms at TPB 1 vs 0.68 ms at TPB 2); at 1 block/CU either
-  // way the 7x7 layers gain ~5 % (add_128 0.742 -> 0.710 ms, conv0_res 0.467 -> 0.443 ms)
-  const size_t l1 = halo_lds_bytes(a.hcap, a.BN, 1), l2 = halo_lds_bytes(a.hcap, a.BN, 2);
-  const size_t cap = 160 * 1024;
-  return (a.ntaps >= 4 && l2 <= cap && cap / l2 == cap / l1) ? 2 : 1;
-}
-
-template <bool BF, int HL, int BN, int WM, int WN, int TPB>
+template <bool BF, int HL, int BN, int WM, int WN>
 static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
-  auto k = halo_kernel<BF, HL, BN, WM, WN, TPB>;
-  const size_t lds = halo_lds_bytes(a.hcap, a.BN, TPB);
-  const int maxl = (int)std::min<size_t>(halo_lds_bytes(HL * 128, BN, TPB), 160 * 1024);
+  auto k = halo_kernel<BF, HL, BN, WM, WN>;
+  const size_t lds = halo_lds_bytes(a.hcap, a.BN);
+  const int maxl = (int)halo_lds_bytes(HL * 128, BN);
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
                       true);
   (void)once;
@@ -388,15 +331,11 @@ static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
 
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s) {
   dim3 grid((a.N * a.tiles_h * a.tiles_w + a.IMG - 1) / a.IMG, a.ntiles, a.ksplit);
-  const int tpb = halo_tpb(a);
-#define X(id, HL_, BN_, WM_, WN_)                                                                   \
-  if (cfg == (id)) {                                                                                \
-    if (a.hcap > HL_ * 128) return -1;                                                              \
-    if (dtype == 1)                                                                                 \
-      return tpb == 2 ? launch_halo_t<true, HL_, BN_, WM_, WN_, 2>(a, grid, s)                      \
-                      : launch_halo_t<true, HL_, BN_, WM_, WN_, 1>(a, grid, s);                     \
-    return tpb == 2 ? launch_halo_t<false, HL_, BN_, WM_, WN_, 2>(a, grid, s)                       \
-                    : launch_halo_t<false, HL_, BN_, WM_, WN_, 1>(a, grid, s);                      \
+#define X(id, HL_, BN_, WM_, WN_)                                         \
+  if (cfg == (id)) {                                                      \
+    if (a.hcap > HL_ * 128) return -1;                                    \
+    return dtype == 1 ? launch_halo_t<true, HL_, BN_, WM_, WN_>(a, grid, s) \
+                      : launch_halo_t<false, HL_, BN_, WM_, WN_>(a, grid, s); \
   }
   TPG_HALO_CFGS(X)
 #undef X

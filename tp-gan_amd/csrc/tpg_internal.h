@@ -289,7 +289,7 @@ int wgrad2_cfg(int bm, int bn);
 int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s);
 int launch_epilogue(const EpiArgs& a, hipStream_t s);
 int halo_cfg(int hl, int bn);
-size_t halo_lds_bytes(int hcap, int bn, int tpb);
+size_t halo_lds_bytes(int hcap, int bn);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
