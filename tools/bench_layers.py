@@ -22,6 +22,8 @@ from tpgan_lib import ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, check,
 # name: (N, Cin, H, W, Cout, k, stride, pad, transposed, output_padding, act, residual)
 SHAPES = {
     "enhance_128": (32, 206, 128, 128, 206, 5, 1, 2, False, 0, ACT_LEAKY, True),
+    "e128_nores": (32, 206, 128, 128, 206, 5, 1, 2, False, 0, ACT_LEAKY, False),
+    "e128_plain": (32, 206, 128, 128, 206, 5, 1, 2, False, 0, ACT_NONE, False),
     "add_128": (32, 75, 128, 128, 75, 7, 1, 3, False, 0, ACT_LEAKY, True),
     "conv0_res": (32, 64, 128, 128, 64, 7, 1, 3, False, 0, ACT_LEAKY, True),
     "conv5_0": (32, 206, 128, 128, 64, 5, 1, 2, False, 0, ACT_LEAKY, False),
@@ -70,8 +72,8 @@ def run(name, s, iters, passes):
     wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
     wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
     calls = {
-        "fwd": lambda: check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w), b.data_ptr(), tt(res), tt(y),
-                                                wsf.data_ptr(), wsf.numel(), stream_ptr())),
+        "fwd": lambda: check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w), b.data_ptr() if act else None,
+                                                tt(res), tt(y), wsf.data_ptr(), wsf.numel(), stream_ptr())),
         "dgrad": lambda: check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w), tt(dx), wsd.data_ptr(),
                                                        wsd.numel(), stream_ptr())),
         "wgrad": lambda: check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0,

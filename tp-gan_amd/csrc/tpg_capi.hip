@@ -265,6 +265,8 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   h.TH = bth; h.TW = btw; h.IMG = bimg; h.SH = 1; h.SW = 1;
   h.HH = bth + sy - 1; h.HW = btw + sx - 1;
   h.hcap = hcap;
+  static const int halo_var = getenv("TPG_HALO_VAR") ? atoi(getenv("TPG_HALO_VAR")) : 0;  // tuning
+  h.var = halo_var;
   for (int t = 0; t < a.ntaps; ++t) h.toff[t] = (a.dy[t] - dymin) * h.HW + (a.dx[t] - dxmin);
   h.pad_mode = a.pad_mode;
   h.N = N; h.JH = JH; h.JW = JW;
@@ -481,6 +483,9 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
       h.R = R.data; h.r_sn = R.stride[0]; h.r_sh = R.stride[2]; h.r_sw = R.stride[3];
       h.res_scale = res_scale; h.act = act; h.slope = slope;
       h.ws = h.ksplit > 1 ? reinterpret_cast<float*>(sk) : nullptr;
+      h.yvec = vec_ok(Y, dtype);
+      h.rvec = R.data ? vec_ok(R, dtype) : 0;
+      h.wvec = a.Nout % 4 == 0;
       int e = launch_halo(h, dtype, P.hcfg, s);
       if (e) return hip_check(e, "halo conv");
       if (h.ksplit > 1) {

@@ -35,6 +35,9 @@ typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 __device__ __forceinline__ int hswz(int row) { return ((row >> 2) & 1) << 1; }
 
 __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 128; }
+// epilogue: rows of the 256-row tile parked in LDS per pass (fp32, stride BN + 4)
+__host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 96 ? 128 : 256; }
+__host__ __device__ constexpr int halo_epi_lds(int bn) { return 256 * 20 + halo_epi_rows(bn) * (bn + 4) * 4; }
 
 // mask_chunk on a native 4 x u32 vector (first-class value: stays in VGPRs)
 template <int EPC>
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const int hcap = p.hcap;
-  constexpr int RS = 3;                                // weight ring slots (one tap slice each)
+  const int RS = (p.var & 2) ? 4 : 3;                  // weight ring slots (one tap slice each)
   u32x4* halo = lds;                                   // [2][hcap][4]
   u32x4* wts = lds + 2 * hcap * 4;                     // [RS][BNL][4] ring
   int* s_toff = reinterpret_cast<int*>(wts + RS * BNL * 4);  // [TPG_MAX_TAPS]
@@ -224,7 +227,32 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   const int ntaps = p.ntaps;
   const int total = nks * ntaps;
   __syncthreads();  // tap table
-  if (total > 0) {
+  if ((p.var & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (total > 0 && RS == 4) {
+    // 4-slot ring: step s+3's weights are issued at the start of step s
+    load_halo(0);
+    issue_w(0, 0);
+    issue_w(min(1, total - 1), 1);
+    issue_w(min(2, total - 1), 2);
+    store_halo(0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    int ks = 0, t = 0, slot = 0;
+    int toff = s_toff[0];
+    for (int s = 0; s < total; ++s) {
+      const bool more_ks = ks + 1 < nks;
+      if (t == 0 && more_ks) load_halo(ks + 1);
+      issue_w(min(s + 3, total - 1), (slot + 3) & 3);
+      const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];
+      compute(ks & 1, slot, toff);
+      toff = toff_next;
+      if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
+      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      slot = (slot + 1) & 3;
+      if (++t == ntaps) { t = 0; ++ks; }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (total > 0) {
     load_halo(0);
     issue_w(0, 0);
     issue_w(min(1, total - 1), 1);
@@ -249,45 +277,142 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
   }
 
-  // ---- epilogue: fused bias / residual / activation store, or an fp32 partial slice
+  // ---- epilogue through LDS: the fp32 accumulators of RP rows at a time are parked in LDS,
+  // then every thread finishes 8-channel groups of whole pixel rows: bias, residual and
+  // activation with 16-byte residual loads / output stores (or an fp32 partial slice row).
+  // Row addresses are computed once per block into a table.
+  constexpr int RP = halo_epi_rows(BN);      // rows per pass (a whole number of wave row-blocks)
+  constexpr int LDW = BN + 4;                // padded fp32 row stride
+  constexpr int CG = BN / 8;                 // 8-channel groups per row
+  constexpr int IPT = RP * CG / 512;         // groups per thread per pass
+  constexpr int NV = 8 * (int)sizeof(E) / 16;  // 16-byte vectors per group
+  static_assert(RP * CG % 512 == 0 && RP % WTM == 0, "epilogue tiling");
+  __syncthreads();                           // every wave is done with the halo and the ring
+  int64_t* s_off = reinterpret_cast<int64_t*>(lds);           // [256][2] out / residual offsets
+  float* s_bias = reinterpret_cast<float*>(lds) + 256 * 4;    // [256] bias of this block's columns
+  float* s_acc = reinterpret_cast<float*>(lds) + 256 * 5;     // [RP][LDW]
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
   float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
-#pragma unroll
-  for (int m = 0; m < MREP; ++m) {
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int q = wm * WTM + m * 16 + 4 * g + reg;
-      const int sub = q / THW, rem = q - sub * THW;
-      const int st = st0 + sub;
-      if (sub >= IMG || st >= ntot) continue;
+  if (tid < BM) {
+    const int q = tid;
+    const int sub = q / THW, rem = q - sub * THW;
+    const int st = st0 + sub;
+    int64_t yo = -1, ro = 0;
+    if (sub < IMG && st < ntot) {
       const int nimg = st / tiles, trem = st - nimg * tiles;
       const int tty = trem / tiles_w, ttx = trem - tty * tiles_w;
       const int ty = rem / TW, tx = rem - ty * TW;
       const int j = tty * TH + ty, i = ttx * TW + tx;
-      if (j >= p.JH || i >= p.JW) continue;
-      if (W) {
-        float* wr = W + ((int64_t)(nimg * p.JH + j) * p.JW + i) * p.Nout;
-#pragma unroll
-        for (int nr = 0; nr < NREP; ++nr) {
-          const int col = n0 + wn * WTN + nr * 16 + l16;
-          if (col < p.Nout) wr[col] = acc[m][nr][reg];
+      if (j < p.JH && i < p.JW) {
+        if (W) {
+          yo = ((int64_t)(nimg * p.JH + j) * p.JW + i) * p.Nout;
+        } else {
+          const int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
+          yo = (int64_t)nimg * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
+          ro = (int64_t)nimg * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
         }
-        continue;
-      }
-      const int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
-      const int64_t yoff = (int64_t)nimg * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
-      const int64_t roff = (int64_t)nimg * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
-#pragma unroll
-      for (int nr = 0; nr < NREP; ++nr) {
-        const int col = n0 + wn * WTN + nr * 16 + l16;
-        if (col >= p.Nout) continue;
-        float v = acc[m][nr][reg];
-        if (p.bias) v += p.bias[col];
-        if (R) v += p.res_scale * (float)R[roff + col];
-        Y[yoff + col] = (E)h_act(v, p.act, p.slope);
       }
     }
+    s_off[2 * q] = yo;
+    s_off[2 * q + 1] = ro;
+  } else if (tid < BM + BN) {
+    const int c = n0 + tid - BM;
+    s_bias[tid - BM] = (p.bias && c < p.Nout) ? p.bias[c] : 0.f;
+  }
+#pragma unroll 1
+  for (int pass = 0; pass < BM / RP; ++pass) {
+    if (wm * WTM >= pass * RP && wm * WTM < (pass + 1) * RP) {
+      float* base = s_acc + (wm * WTM - pass * RP + 4 * g) * LDW + wn * WTN + l16;  // constant offsets below
+#pragma unroll
+      for (int m = 0; m < MREP; ++m)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+          for (int n = 0; n < NREP; ++n) base[(m * 16 + reg) * LDW + n * 16] = acc[m][n][reg];
+    }
+    __syncthreads();
+    if (W) {  // split-K partial slice rows (fp32, row stride Nout)
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int it = tid + 512 * k;
+        const int row = it / CG, c0 = (it - row * CG) * 8;
+        const int64_t yo = s_off[2 * (pass * RP + row)];
+        const int col0 = n0 + c0;
+        const int ncol = min(8, p.Nout - col0);
+        if (yo < 0 || ncol <= 0) continue;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0 + 4);
+        float* dst = W + yo + col0;
+        if (ncol == 8 && p.wvec) {
+          *reinterpret_cast<f32x4*>(dst) = a0;
+          *reinterpret_cast<f32x4*>(dst + 4) = a1;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (e < ncol) dst[e] = e < 4 ? a0[e & 3] : a1[e & 3];
+        }
+      }
+    } else {
+      // residual vectors of every group first (all loads in flight), then finish and store
+      // (bf16; the fp32 parity mode loads them in the finishing loop: register budget)
+      constexpr int PF = BF ? IPT : 0;
+      u32x4 rv[IPT][NV];
+#pragma unroll
+      for (int k = 0; k < (R ? PF : 0); ++k) {
+        const int it = tid + 512 * k;
+        const int row = it / CG, c0 = (it - row * CG) * 8;
+        // unconditional (clamped) loads so that all of them issue before the first wait
+        const bool ok = p.rvec && p.Nout - (n0 + c0) >= 8 && s_off[2 * (pass * RP + row)] >= 0;
+        const u32x4* src = reinterpret_cast<const u32x4*>(R + (ok ? s_off[2 * (pass * RP + row) + 1] + n0 + c0 : 0));
+#pragma unroll
+        for (int v = 0; v < NV; ++v) rv[k][v] = src[v];
+      }
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int it = tid + 512 * k;
+        const int row = it / CG, c0 = (it - row * CG) * 8;
+        const int64_t yo = s_off[2 * (pass * RP + row)];
+        const int col0 = n0 + c0;
+        const int ncol = min(8, p.Nout - col0);
+        if (yo < 0 || ncol <= 0) continue;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0 + 4);
+        float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        {
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + c0);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + c0 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[e] += b0[e]; v[e + 4] += b1[e]; }
+        }
+        const bool full = ncol == 8;
+        if (R) {
+          union { u32x4 u[NV]; E e[8]; } rr;
+#pragma unroll
+          for (int q = 0; q < NV; ++q) rr.u[q] = rv[k][q];
+          if (!(full && p.rvec && BF)) {
+            const E* rs = R + s_off[2 * (pass * RP + row) + 1] + col0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) rr.e[e] = e < ncol ? rs[e] : (E)0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += p.res_scale * (float)rr.e[e];
+        }
+        union { u32x4 u[NV]; E e[8]; } o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.e[e] = (E)h_act(v[e], p.act, p.slope);
+        E* dst = Y + yo + col0;
+        if (full && p.yvec) {
+#pragma unroll
+          for (int q = 0; q < NV; ++q) reinterpret_cast<u32x4*>(dst)[q] = o.u[q];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (e < ncol) dst[e] = o.e[e];
+        }
+      }
+    }
+    if (pass + 1 < BM / RP) __syncthreads();  // before the next pass overwrites s_acc
   }
 }
 
@@ -313,15 +438,15 @@ int halo_cfg(int hl, int bn) {
 // Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
 // 7x7 layers alone, -2 % on the train step) and a cross-barrier fragment prefetch with a
 // 4-slot ring (-2..12 %: the second fragment set pushed the 224-wide tile past 256 VGPRs).
-size_t halo_lds_bytes(int hcap, int bn) {
-  return (size_t)(2 * hcap * 4 + 3 * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
+size_t halo_lds_bytes(int hcap, int bn, int rs) {
+  return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn));
 }
 
 template <bool BF, int HL, int BN, int WM, int WN>
 static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
   auto k = halo_kernel<BF, HL, BN, WM, WN>;
-  const size_t lds = halo_lds_bytes(a.hcap, a.BN);
-  const int maxl = (int)halo_lds_bytes(HL * 128, BN);
+  const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3);
+  const int maxl = (int)halo_lds_bytes(HL * 128, BN, 4);
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
                       true);
   (void)once;

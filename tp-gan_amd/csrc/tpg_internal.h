@@ -271,6 +271,9 @@ struct HaloArgs {
   float res_scale;
   int act;
   float slope;
+  int yvec, rvec, wvec;       // 16-byte output / residual / partial-slice stores allowed
+  int var;                    // pipeline variant bits (TPG_HALO_VAR, tuning): 1 = waves 4-7 at
+                              // priority 1, 2 = 4-slot weight ring (DMA three steps ahead)
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 
@@ -289,7 +292,7 @@ int wgrad2_cfg(int bm, int bn);
 int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s);
 int launch_epilogue(const EpiArgs& a, hipStream_t s);
 int halo_cfg(int hl, int bn);
-size_t halo_lds_bytes(int hcap, int bn);
+size_t halo_lds_bytes(int hcap, int bn, int rs = 3);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
