@@ -81,7 +81,10 @@ typedef struct tpg_conv_desc {
   float res_scale;                /* ResidualBlock scaling_factor (ModificationLayer.py:300) */
   int32_t ksplit;                 /* 0 = automatic; >= 1 forces the K split (bwd_filter: pixel splits) */
   int32_t algo;                   /* 0 = automatic; bwd_filter: 1..5 = tile 256x128, 128x128, 128x64,
-                                     64x128, 64x64 (used with ksplit >= 1; autotuners set both) */
+                                     64x128, 64x64 (used with ksplit >= 1; autotuners set both);
+                                     6..9 = kernel-row halo kernel, tile 128x64, 128x32, 64x64,
+                                     64x32 (stride-1 bf16 Conv2d, 3/5/7-wide kernels, output
+                                     width a multiple of 64; -30 otherwise) */
   int32_t flags;                  /* TPG_FLAG_*: WPACKED = w.data is the image tpg_conv2d_pack_jobs /
                                      tpg_pack_run produced for this descriptor and op */
 } tpg_conv_desc;

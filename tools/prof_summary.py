@@ -53,6 +53,22 @@ def main():
         e[3] = min(e[3], dur)
     total = sum(v[1] for v in agg.values())
     span = (rows[-1][1] - rows[0][0]) if rows else 0
+    # union of kernel intervals (streams overlap) and the idle gaps between them
+    busy, cur0, cur1, gaps = 0, None, None, collections.Counter()
+    for t0, t1, name in rows:
+        if cur1 is None or t0 > cur1:
+            if cur1 is not None:
+                busy += cur1 - cur0
+                g = t0 - cur1
+                gaps["<5us" if g < 5000 else "5-20us" if g < 20000 else "20-100us" if g < 100000 else ">100us"] += g
+            cur0, cur1 = t0, t1
+        else:
+            cur1 = max(cur1, t1)
+    if cur1 is not None:
+        busy += cur1 - cur0
+    print("GPU busy (union) %.2f ms/step, idle %.2f ms/step; idle by gap size: %s" % (
+        busy / 1e6 / steps, (span - busy) / 1e6 / steps,
+        ", ".join("%s %.2f ms" % (k, v / 1e6 / steps) for k, v in sorted(gaps.items()))))
     items = sorted(agg.items(), key=lambda kv: -kv[1][1])
     print("steps in window: %d   kernel time %.2f ms/step   wall span %.2f ms/step   (busy %.1f%%)" % (
         steps, total / 1e6 / steps, span / 1e6 / steps, 100 * total / max(span, 1)))

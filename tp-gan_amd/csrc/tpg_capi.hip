@@ -669,6 +669,72 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
                    "reflect_fold");
 }
 
+// Row-halo weight gradient (tpg_wgrad_rh.hip) for a stride-1 Conv2d: returns 1 when the
+// shape is not covered (caller falls back), else the launch status.
+static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_tensor& g, const tpg_tensor& dw,
+                        hipStream_t stream) {
+  if (d->dtype != TPG_BF16 || d->stride_h != 1 || d->stride_w != 1) return 1;
+  if (d->kw != 3 && d->kw != 5 && d->kw != 7) return 1;
+  const int PH = d->out_h, PW = d->out_w, QH = d->in_h, QW = d->in_w;
+  if (PW % 64 || d->pad_t >= QH || d->pad_l >= QW || !vec_ok(g, d->dtype) || !vec_ok(x, d->dtype)) return 1;
+  if (g.stride[2] != (int64_t)PW * g.stride[3] || g.stride[0] != (int64_t)PH * g.stride[2]) return 1;
+  if (x.stride[2] != (int64_t)QW * x.stride[3] || x.stride[0] != (int64_t)QH * x.stride[2]) return 1;
+  // extents cover the last pixel's whole 16-byte chunks (vec_ok: pixel stride >= ceil8(C))
+  const int64_t pb = ((int64_t)(d->n - 1) * g.stride[0] + (int64_t)(PH - 1) * g.stride[2] +
+                      (int64_t)(PW - 1) * g.stride[3] + rup(d->out_c, 8)) * 2;
+  const int64_t qb = ((int64_t)(d->n - 1) * x.stride[0] + (int64_t)(QH - 1) * x.stride[2] +
+                      (int64_t)(QW - 1) * x.stride[3] + rup(d->in_c, 8)) * 2;
+  if (pb >= (1ll << 31) || qb >= (1ll << 31)) return 1;
+  WgradRHArgs a;
+  memset(&a, 0, sizeof(a));
+  a.P = g.data; a.p_sn = (int)g.stride[0]; a.p_sh = (int)g.stride[2]; a.p_sw = (int)g.stride[3];
+  a.PH = PH; a.PW = PW; a.Ca = d->out_c; a.p_bytes = (int)pb;
+  a.Q = x.data; a.q_sn = (int)x.stride[0]; a.q_sh = (int)x.stride[2]; a.q_sw = (int)x.stride[3];
+  a.QH = QH; a.QW = QW; a.Cb = d->in_c; a.q_bytes = (int)qb;
+  a.kh = d->kh; a.kw = d->kw; a.pt = d->pad_t; a.pl = d->pad_l; a.pad_mode = d->pad_mode;
+  a.nt = d->kw == 7 ? 4 : d->kw;
+  // tile: fewest padded MACs, the 128 x 64 tile (best operand reuse) on ties
+  int bm = 128, bc = 64;
+  if (d->algo >= 6 && d->algo <= 9) {
+    a.cfg = d->algo - 6;
+    wgrad_rh_tile(a.cfg, &bm, &bc);
+  } else {
+    int64_t best = -1;
+    for (int c = 0; c < 4; ++c) {
+      int m, b;
+      wgrad_rh_tile(c, &m, &b);
+      const int64_t cost = rup(a.Ca, m) * rup(a.Cb, b) * (100 + (m == 64 ? 8 : 0) + (b == 32 ? 8 : 0));
+      if (best < 0 || cost < best) { best = cost; a.cfg = c; bm = m; bc = b; }
+    }
+  }
+  a.nta = cdiv(a.Ca, bm); a.ntb = cdiv(a.Cb, bc);
+  a.tiles = a.nta * a.ntb * a.kh * cdiv(a.kw, a.nt);
+  a.nkt = d->n * PH * (PW / 64);
+  int ks = 1;
+  if (d->algo >= 6 && d->ksplit >= 1) {
+    ks = d->ksplit;
+  } else {
+    // pixel splits: whole rounds of resident blocks (one per CU, two for the <= 128-VGPR
+    // tiles) against the fp32 atomics every extra split adds (~1.3 TB/s of added bytes)
+    const int resident = (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256;
+    const double flops = 2.0 * a.tiles * bm * a.nt * bc * 64.0 * a.nkt;
+    double best = -1;
+    for (int k = 1; k <= 64 && k <= a.nkt; ++k) {
+      const int64_t blocks = (int64_t)a.tiles * k;
+      const double rounds = (double)((blocks + resident - 1) / resident);
+      const double t = rounds * flops / blocks / (4.5e12 * 256 / resident) +
+                       (k > 1 ? k * (double)a.tiles * bm * a.nt * bc * 4 / 1.3e12 : 0.0);
+      if (best < 0 || t < best) { best = t; ks = k; }
+    }
+  }
+  ks = std::max(1, std::min(ks, a.nkt));
+  a.kt_per_split = cdiv(a.nkt, ks);
+  a.ksplit = cdiv(a.nkt, a.kt_per_split);
+  a.dW = reinterpret_cast<float*>(dw.data);
+  a.w_sa = dw.stride[0]; a.w_sb = dw.stride[1]; a.w_sr = dw.stride[2]; a.w_ss = dw.stride[3];
+  return hip_check(launch_wgrad_rh(a, stream), "wgrad_rh");
+}
+
 extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw, void* ws,
                                          size_t ws_bytes, tpg_stream_t stream) {
   (void)ws; (void)ws_bytes;
@@ -712,6 +778,15 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   a.w_sa = dw.stride[0]; a.w_sb = dw.stride[1]; a.w_sr = dw.stride[2]; a.w_ss = dw.stride[3];
   a.div_pw.init(a.PW);
   a.div_phpw.init(a.PH * a.PW);
+  // kernel-row halo kernel (stride-1 Conv2d, bf16, 64-pixel row segments): algo 6, and the
+  // default for untuned calls when it applies
+  static const bool rh_on = !getenv("TPG_WGRAD_RH") || atoi(getenv("TPG_WGRAD_RH")) != 0;  // A/B hook
+  const bool rh_algo = d->algo >= 6 && d->algo <= 9;
+  if (((d->algo == 0 && rh_on) || rh_algo) && !comp && !d->transposed) {
+    const int rc = wgrad_rh(d, x, g, dw, (hipStream_t)stream);
+    if (rc != 1) return rc;
+  }
+  if (rh_algo) return fail(-30, "wgrad: row-halo kernel does not apply to this shape");
   // pipelined DMA kernel when both operands are 16-byte aligned channels-last rows
   if (a.vec_p && a.vec_q) {
     // non-composite: columns flattened over taps (b' = tap * rup(Cb, 8) + b), so channel
@@ -750,8 +825,11 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
     a.pix_per_split = (int)rup(cdiv(a.npix, bks), kp);
     a.ksplit = cdiv(a.npix, a.pix_per_split);
     const int es = esize(d->dtype);
+    // byte extent up to the end of the last pixel's last 16-byte chunk (a chunk straddling C
+    // must not count as out of range: vec_ok rows are padded to whole chunks)
     auto extent = [&](const tpg_tensor& t, int n, int h, int w, int c) -> int64_t {
-      return ((int64_t)(n - 1) * t.stride[0] + (int64_t)(h - 1) * t.stride[2] + (int64_t)(w - 1) * t.stride[3] + c) * es;
+      return ((int64_t)(n - 1) * t.stride[0] + (int64_t)(h - 1) * t.stride[2] + (int64_t)(w - 1) * t.stride[3] +
+              rup(c, 16 / es)) * es;
     };
     const int64_t pb = extent(P, d->n, a.PH == 1 && comp ? 1 : PH, a.PW == 1 && comp ? 1 : PW, a.Ca);
     const int64_t qb = comp ? extent(Q, d->n, 1, 1, a.Cb) : extent(Q, d->n, QH, QW, cb);

@@ -124,6 +124,22 @@ struct WgradArgs {
 };
 typedef WgradArgs Wgrad2Args;
 
+// Stride-1 Conv2d weight gradient by kernel-row halos (tpg_wgrad_rh.hip): P = dY, Q = X,
+// both dense channels-last; element strides; byte extents < 2^31.
+struct WgradRHArgs {
+  const void* P;
+  int p_sn, p_sh, p_sw, PH, PW, Ca, p_bytes;
+  const void* Q;
+  int q_sn, q_sh, q_sw, QH, QW, Cb, q_bytes;
+  int kh, kw, pt, pl, pad_mode;
+  int nt;                     // taps per block (3, 4, 5); groups = ceil(kw / nt)
+  int cfg;                    // tile: 0 = 128 x 64, 1 = 128 x 32, 2 = 64 x 64, 3 = 64 x 32 (a x b)
+  int nta, ntb, tiles;        // tiles = nta * ntb * kh * groups
+  int nkt, kt_per_split, ksplit;
+  float* dW;
+  int64_t w_sa, w_sb, w_sr, w_ss;
+};
+
 // ---------------------------------------------------------------- weight packing ----
 // Wp[n'][unit*16 + e] = W[a][b][r][s] (fp32 master -> compute dtype, zero padded).
 // n' and c' = (unit % upt)*16 + e decode by mode: 0 -> a, 1 -> b, 2 -> composite (r,s,b),
@@ -291,6 +307,8 @@ int launch_pack(const PackArgs& a, hipStream_t s);
 int wgrad2_cfg(int bm, int bn);
 int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s);
 int launch_epilogue(const EpiArgs& a, hipStream_t s);
+int launch_wgrad_rh(const WgradRHArgs& a, hipStream_t s);
+int wgrad_rh_tile(int cfg, int* bm, int* bc);
 int halo_cfg(int hl, int bn);
 size_t halo_lds_bytes(int hcap, int bn, int rs = 3);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);

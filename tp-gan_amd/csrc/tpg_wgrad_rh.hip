@@ -1,0 +1,287 @@
+// Weight gradient of a stride-1 Conv2d by kernel-row halos (gfx950, bf16):
+//   dW[a][b][r][s] += sum_{n,py,px} dY[n][py][px][a] * X[n][py + r - pt][px + s - pl][b].
+//
+// tpg_wgrad2.hip flattens (tap, b) into GEMM columns, so every 64-pixel k-tile DMAs the dY
+// tile once per 128-column tile and the X pixels once per TAP: for a 5x5 206-channel layer
+// at 128x128 that is ~16 GB of LDS-DMA per call and the kernel runs at the chip's DMA-fill
+// rate, not the MFMA rate.  Here a block owns one kernel row r and a group of NT horizontal
+// taps s0..s0+NT-1 (GEMM columns = NT x 64 channels), and a k-tile is 64 consecutive
+// pixels of ONE image row, so the X operand of all NT taps is a single row segment of
+// 64 + NT - 1 halo pixels, loaded once; tap s reads it shifted by s rows in LDS.  Bytes per
+// flop drop ~2.4x (dY 16 KB + X 9 KB per 5.2 MFLOP at NT = 5).
+//
+// Pipeline as in wgrad2: 8 waves, both operands by buffer LDS-DMA (out-of-range offsets read
+// zero = padding), 3-stage ring two k-tiles ahead, one counted vmcnt + barrier per k-tile,
+// ds_read_b64_tr_b16 fragment reads for v_mfma_f32_16x16x32_bf16, fp32 atomics over the
+// pixel splits.  Blocks of one pixel split are adjacent in the XCD-aware order, so the
+// tiles that read the same dY / X rows run together on one XCD's L2.
+#include "tpg_internal.h"
+
+namespace tpg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ s16x4 rh_tr_read(const char* p) {
+  s16x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+// chunk swizzles of the LDS rows (256- and 128-byte rows as in tpg_wgrad2.hip; 64-byte rows:
+// the g = 0 / 1 row octets of a transposed read use disjoint chunk pairs)
+template <int RB>
+__device__ __forceinline__ int rh_swz(int row) {
+  if constexpr (RB == 256) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  else if constexpr (RB == 128) return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;
+  else return ((row >> 3) & 1) << 1;
+}
+
+__device__ __forceinline__ int rh_refl(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+template <int NT, int BM, int BC>
+__global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
+  constexpr int KP = 64;                     // pixels per k-tile (one image-row segment)
+  // BM a (dY channels) x BC b (X channels) per block; GEMM columns: (tap, b)
+  constexpr int BN = NT * BC;
+  constexpr int WM = (BM == 64 && BC == 64) ? 2 : 4, WN = 8 / WM;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MREP = WTM / 16, NREP = WTN / 16;
+  constexpr int RBA = BM * 2, RBB = BC * 2;  // LDS row bytes
+  constexpr int BYTES_A = KP * RBA;
+  constexpr int GA = BYTES_A / 8192;         // 1 KiB DMA pieces per wave for dY
+  constexpr int HROWS = 72;                  // >= KP + NT - 1 halo pixels
+  constexpr int BYTES_B = HROWS * RBB;
+  constexpr int PB = (BYTES_B + 1023) / 1024, GB = (PB + 7) / 8;  // X pieces, per wave
+  constexpr int RPP = 1024 / RBA, RPB = 1024 / RBB;              // rows per piece
+  constexpr int STAGE = BYTES_A + GB * 8 * 1024;
+  static_assert(NT >= 3 && NT <= 5 && KP + NT - 1 <= HROWS, "taps per block");
+  static_assert(GA * 8192 == BYTES_A && GA >= 1 && GB <= 2, "dma pieces");
+  static_assert(MREP * 16 * WM == BM && NREP * 16 * WN == BN, "waves");
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [3][STAGE]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+  // XCD-aware block order: physical block b runs on XCD b % 8 and each XCD is handed a
+  // contiguous range of logical blocks; logical = split * tiles + tile.
+  const int nblk = gridDim.x, full = nblk & ~7, bid = blockIdx.x;
+  const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
+  const int tile = L % p.tiles, split = L / p.tiles;
+  int t = tile;
+  const int ta = t % p.nta; t /= p.nta;
+  const int tb = t % p.ntb; t /= p.ntb;
+  const int r = t % p.kh;
+  const int grp = t / p.kh;
+  const int a0 = ta * BM, b0 = tb * BC, s0 = grp * NT;
+  const int kt0 = split * p.kt_per_split;
+  const int nkt = min(p.nkt, kt0 + p.kt_per_split) - kt0;
+  if (nkt <= 0) return;
+
+  // position of k-tile kt0: (n, py, px0), advanced incrementally (all scalar)
+  const int segs = p.PW / KP;
+  int n = kt0 / (p.PH * segs);
+  int rem = kt0 - n * p.PH * segs;
+  int py = rem / segs;
+  int px0 = (rem - py * segs) * KP;
+
+  const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.P), 0, p.p_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Q), 0, p.q_bytes, 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+
+  // per-lane constants of the DMA pieces
+  //   dY piece j of wave w: tile rows (GA*w + j) * RPP .. +RPP-1
+  unsigned aoff[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int row = (wave * GA + j) * RPP + lane / (RBA / 16), pc = lane % (RBA / 16);
+    const int c = a0 + ((pc ^ rh_swz<RBA>(row)) << 3);
+    aoff[j] = c < p.Ca ? (unsigned)((row * p.p_sw + c) * 2) : OOB;
+  }
+  //   X piece j * 8 + w: halo rows (j * 8 + w) * RPB ..; pieces past PB only pad the count
+  int bhx[GB], bch[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = (j * 8 + wave) * RPB + lane / (RBB / 16), pc = lane % (RBB / 16);
+    const int c = b0 + ((pc ^ rh_swz<RBB>(row)) << 3);
+    bhx[j] = row - p.pl + s0;                  // + px0 = X column of this halo pixel
+    bch[j] = (c < p.Cb && row < KP + NT - 1 && j * 8 + wave < PB) ? c : -1;
+  }
+
+  auto issue = [&](int slot, int n_, int py_, int px_) {
+    char* st = lds + slot * STAGE;
+    const int sbase = (n_ * p.p_sn + py_ * p.p_sh + px_ * p.p_sw) * 2;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      // (a local copy: hipcc silently drops the kernel's host stub when the dependent-size
+      // array element goes into the builtin directly)
+      const unsigned vo = aoff[j];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(st + (wave * GA + j) * 1024),
+                                               16, vo, sbase, 0, 0);
+    }
+    int qy = py_ + r - p.pt;
+    bool yok = (unsigned)qy < (unsigned)p.QH;
+    if (p.pad_mode) { qy = rh_refl(qy, p.QH); yok = true; }
+    const int qbase = (n_ * p.q_sn + qy * p.q_sh) * 2;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      int qx = px_ + bhx[j];
+      bool ok = yok && bch[j] >= 0;
+      if (p.pad_mode) qx = rh_refl(qx, p.QW);
+      else ok = ok && (unsigned)qx < (unsigned)p.QW;
+      const unsigned off = ok ? (unsigned)((qx * p.q_sw + bch[j]) * 2) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (__attribute__((address_space(3))) void*)(st + BYTES_A + (j * 8 + wave) * 1024),
+                                               16, off, yok ? qbase : 0, 0, 0);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int q = l16 >> 2, p4 = l16 & 3;
+  f32x4 acc[MREP][NREP];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Fragment reads (transposed, 4 channels x 4 pixels per lane and read): fragment r < 2*MREP
+  // is dY (A), the rest X halo rows shifted by the column's tap.  Next substep's reads are
+  // issued between this substep's MFMAs (as in wgrad2).
+  auto compute = [&](int slot) {
+    const char* A = lds + slot * STAGE;
+    const char* B = A + BYTES_A;
+    constexpr int NS = KP / 32;
+    constexpr int R = 2 * (MREP + NREP), M = MREP * NREP;
+    auto addr = [&](int ks, int rr) -> const char* {
+      if (rr < 2 * MREP) {
+        const int col = wm * WTM + (rr >> 1) * 16 + 4 * p4;
+        const int row = ks * 32 + 8 * g + 4 * (rr & 1) + q;
+        return A + row * RBA + (((col >> 3) ^ rh_swz<RBA>(row)) << 4) + (col & 7) * 2;
+      }
+      const int r2 = rr - 2 * MREP;
+      const int col = wn * WTN + (r2 >> 1) * 16 + 4 * p4;  // (tap, b) column
+      const int tap = col / BC, cb = col % BC;
+      const int row = ks * 32 + 8 * g + 4 * (r2 & 1) + q + tap;
+      return B + row * RBB + (((cb >> 3) ^ rh_swz<RBB>(row)) << 4) + (cb & 7) * 2;
+    };
+    s16x4 h[2][R];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) h[0][rr] = rh_tr_read(addr(0, rr));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < NS; ++ks) {
+      const int cur = ks & 1;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int m = i / NREP, j = i % NREP;
+        const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
+                                                                             0, 1, 2, 3, 4, 5, 6, 7));
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * j],
+                                                                             h[cur][2 * MREP + 2 * j + 1],
+                                                                             0, 1, 2, 3, 4, 5, 6, 7));
+        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[m][j], 0, 0, 0);
+        if (ks + 1 < NS) {
+#pragma unroll
+          for (int rr = i * R / M; rr < (i + 1) * R / M; ++rr) h[cur ^ 1][rr] = rh_tr_read(addr(ks + 1, rr));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ks + 1 < NS) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // pipeline: k-tile i in ring slot i % 3, issued two k-tiles ahead (clamped: static vmcnt)
+  int in_ = n, iy = py, ix = px0, issued = 0;  // position of the next k-tile to issue
+  auto issue_next = [&](int slot) {
+    issue(slot, in_, iy, ix);
+    if (++issued < nkt) {
+      ix += KP;
+      if (ix == p.PW) { ix = 0; if (++iy == p.PH) { iy = 0; ++in_; } }
+    }
+  };
+#define RH_WAIT_BARRIER()                                                                          \
+  do {                                                                                             \
+    if constexpr (GA + GB == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else if constexpr (GA + GB == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
+  } while (0)
+  static_assert(GA + GB >= 2 && GA + GB <= 4, "vmcnt");
+  issue_next(0);
+  issue_next(1);
+  RH_WAIT_BARRIER();  // retires k-tile 0
+  int slot = 0;
+  for (int kt = 0; kt < nkt; ++kt) {
+    issue_next(slot == 0 ? 2 : slot - 1);
+    compute(slot);
+    RH_WAIT_BARRIER();  // retires k-tile kt+1, kt+2 stays in flight
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+#undef RH_WAIT_BARRIER
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- epilogue: fp32 atomics (plain read-add-write without a pixel split)
+#pragma unroll
+  for (int m = 0; m < MREP; ++m)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int a = a0 + wm * WTM + m * 16 + 4 * g + reg;
+      if (a >= p.Ca) continue;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const int col = wn * WTN + j * 16 + l16;
+        const int s = s0 + col / BC, b = b0 + col % BC;
+        if (s >= p.kw || b >= p.Cb) continue;
+        float* dst = p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss;
+        if (p.ksplit == 1) *dst += acc[m][j][reg];
+        else atomicAdd(dst, acc[m][j][reg]);
+      }
+    }
+}
+
+// tile configs {id, BM, BC}; id = desc.algo - 6
+#define TPG_WGRAD_RH_CFGS(X) \
+  X(0, 128, 64)              \
+  X(1, 128, 32)              \
+  X(2, 64, 64)               \
+  X(3, 64, 32)
+
+int wgrad_rh_tile(int cfg, int* bm, int* bc) {
+#define X(id, BM_, BC_) if (cfg == (id)) { *bm = BM_; *bc = BC_; return 0; }
+  TPG_WGRAD_RH_CFGS(X)
+#undef X
+  return -1;
+}
+
+template <int NT, int BM, int BC>
+static int launch_rh_t(const WgradRHArgs& a, hipStream_t s) {
+  constexpr int GB = ((72 * BC * 2 + 1023) / 1024 + 7) / 8;
+  const size_t lds = 3 * (64 * BM * 2 + GB * 8 * 1024);
+  auto k = wgrad_rh_kernel<NT, BM, BC>;
+  static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                      true);
+  (void)once;
+  hipLaunchKernelGGL(k, dim3(a.tiles * a.ksplit), dim3(512), lds, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_wgrad_rh(const WgradRHArgs& a, hipStream_t s) {
+#define X(id, BM_, BC_)                                           \
+  if (a.cfg == (id)) {                                            \
+    if (a.nt == 3) return launch_rh_t<3, BM_, BC_>(a, s);         \
+    if (a.nt == 4) return launch_rh_t<4, BM_, BC_>(a, s);         \
+    if (a.nt == 5) return launch_rh_t<5, BM_, BC_>(a, s);         \
+  }
+  TPG_WGRAD_RH_CFGS(X)
+#undef X
+  return -1;
+}
+
+}  // namespace tpg
