@@ -175,6 +175,39 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Stagger (bf16, BN >= 128 tiles, which run one block per CU anyway; var bit 8 turns it
+  // off): waves 4-7 carry the MFMAs of B fragments NH.. of every step over the barrier
+  // (operands held in registers, +28 VGPRs) and issue them first in the next step, so each
+  // SIMD has matrix work while its partner wave waits for the step's fragment reads
+  // (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Measured ~1 % on the 128x128 layers.
+  constexpr bool LAG_OK = BF && BN >= 128;
+  constexpr int NH = LAG_OK ? (NREP + 1) / 2 : NREP;
+  const bool lag = LAG_OK && !(p.var & 8) && wave >= 4;
+  u32x4 ha[MREP], hb[NREP - NH + 1];
+#pragma unroll
+  for (int m = 0; m < MREP; ++m) ha[m] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int n = 0; n < NREP - NH; ++n) hb[n] = u32x4{0u, 0u, 0u, 0u};
+  auto mma = [&](u32x4 a, u32x4 b, f32x4 c) -> f32x4 {
+    if constexpr (BF) {
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                     0, 0, 0);
+    } else {
+      const f32x4 a4 = __builtin_bit_cast(f32x4, a);
+      const f32x4 b4 = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], c, 0, 0, 0);
+      return c;
+    }
+  };
+  auto held_mfmas = [&]() {
+    if constexpr (LAG_OK)
+#pragma unroll
+    for (int n = NH; n < NREP; ++n)
+#pragma unroll
+      for (int m = 0; m < MREP; ++m) acc[m][n] = mma(ha[m], hb[n - NH], acc[m][n]);
+  };
+
   auto compute = [&](int hbuf, int wslot, int toff) {
     const u32x4* H = halo + hbuf * hcap * 4;
     const u32x4* Wl = wts + wslot * BNL * 4;
@@ -193,27 +226,28 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
       const int r = wn * WTN + n * 16 + l16;
       bf[n] = Wl[r * 4 + (g ^ hswz(r))];
     }
+    if (LAG_OK && lag) {
+      held_mfmas();  // previous step's tail: operands already in registers
 #pragma unroll
-    for (int n = 0; n < NREP; ++n) {
-      const u32x4 bv = bf[n];
+      for (int n = 0; n < NH; ++n)
 #pragma unroll
-      for (int m = 0; m < MREP; ++m) {
-        if constexpr (BF) {
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[m]),
-                                                              __builtin_bit_cast(bf16x8, bv), acc[m][n], 0, 0, 0);
-        } else {
-          const f32x4 a4 = __builtin_bit_cast(f32x4, af[m]);
-          const f32x4 b4 = __builtin_bit_cast(f32x4, bv);
+        for (int m = 0; m < MREP; ++m) acc[m][n] = mma(af[m], bf[n], acc[m][n]);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], acc[m][n], 0, 0, 0);
-        }
-      }
+      for (int m = 0; m < MREP; ++m) ha[m] = af[m];
+#pragma unroll
+      for (int n = NH; n < NREP; ++n) hb[n - NH] = bf[n];
+      __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP, 0);
+    } else {
+#pragma unroll
+      for (int n = 0; n < NREP; ++n)
+#pragma unroll
+        for (int m = 0; m < MREP; ++m) acc[m][n] = mma(af[m], bf[n], acc[m][n]);
+      // schedule: every fragment read first, then the MFMAs (counted lgkmcnt waits instead
+      // of one full wait per B fragment)
+      __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP * (BF ? 1 : 4), 0);
     }
-    // schedule: every fragment read first, then the MFMAs (counted lgkmcnt waits instead
-    // of one full wait per B fragment)
-    __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP * (BF ? 1 : 4), 0);
   };
 
   // Software pipeline over steps s = ks*ntaps + t, one barrier per step:
@@ -276,6 +310,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
   }
+
+  if (lag) held_mfmas();  // the last step's carried MFMAs
 
   // ---- epilogue through LDS: the fp32 accumulators of RP rows at a time are parked in LDS,
   // then every thread finishes 8-channel groups of whole pixel rows: bias, residual and

@@ -289,7 +289,8 @@ struct HaloArgs {
   float slope;
   int yvec, rvec, wvec;       // 16-byte output / residual / partial-slice stores allowed
   int var;                    // pipeline variant bits (TPG_HALO_VAR, tuning): 1 = waves 4-7 at
-                              // priority 1, 2 = 4-slot weight ring (DMA three steps ahead)
+                              // priority 1, 2 = 4-slot weight ring (DMA three steps ahead),
+                              // 8 = no wave stagger (bf16 BN >= 128 tiles stagger waves 4-7)
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 
