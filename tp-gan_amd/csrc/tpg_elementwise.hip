@@ -109,6 +109,55 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(int N, int C, int H, int W
   }
 }
 
+// Row form for pixel-dense channels-last tensors of any alignment, pixel stride and dtype
+// mix (channel slices of concat buffers, fp32 incoming gradients), C <= 256: lane = channel,
+// 256 / C pixel lanes per block, eight pixels per iteration with every load issued first; no
+// index division.  dbias as in the vector form (up to 4096 blocks).
+__global__ __launch_bounds__(256) void act_bwd_rows_kernel(int64_t npix, int C, int act, float slope, tpg_tensor gy,
+                                                           tpg_tensor y, tpg_tensor g, float* dbias,
+                                                           int64_t pix_per_block) {
+  constexpr int U = 8;  // 2- or 4-byte lanes: more pixels in flight than the vector form
+  __shared__ float sb[256];
+  const int ppi = 256 / C;
+  const int c = threadIdx.x % C, pl = threadIdx.x / C;
+  const bool active = pl < ppi;
+  const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
+  if (p0 >= npix) return;  // (uniform) the grid may overshoot by a block
+  const int64_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
+  const bool has_act = act != TPG_ACT_NONE;
+  const int64_t gs = gy.stride[3], ys = y.stride[3], os = g.stride[3];
+  float part = 0.f;
+  if (active) {
+    for (int64_t pb = p0 + pl; pb < p1; pb += (int64_t)U * ppi) {
+      float vg[U], vy[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t pix = pb + (int64_t)u * ppi;
+        const int64_t pc = pix < p1 ? pix : p0;  // clamped: every load issues before any use
+        vg[u] = ld_any(gy.data, gy.dtype, pc * gs + c);
+        vy[u] = has_act ? ld_any(y.data, y.dtype, pc * ys + c) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t pix = pb + (int64_t)u * ppi;
+        if (pix < p1) {
+          const float v = has_act ? tpg_act_grad(vg[u], vy[u], act, slope) : vg[u];
+          st_any(g.data, g.dtype, pix * os + c, v);
+          part += v;
+        }
+      }
+    }
+  }
+  if (!dbias) return;
+  sb[threadIdx.x] = active ? part : 0.f;
+  __syncthreads();
+  if (threadIdx.x < C) {
+    float sum = 0.f;
+    for (int q = 0; q < ppi; ++q) sum += sb[q * C + threadIdx.x];
+    atomicAdd(dbias + threadIdx.x, sum);
+  }
+}
+
 // Vector form for channels-last tensors with pixel-dense, 16-byte aligned rows: a thread
 // owns one 16-byte channel chunk and walks a contiguous pixel range of its block, four
 // pixels per iteration with all loads issued before any use (HBM latency hiding).  Its
@@ -362,6 +411,22 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
 
 using namespace tpg;
 
+// pixel-dense channels-last rows (channel stride 1, any pixel stride / alignment)
+static bool pix_dense_any(const tpg_tensor& t, int h, int w) {
+  return t.stride[1] == 1 && t.stride[2] == t.stride[3] * w && t.stride[0] == t.stride[2] * h;
+}
+
+// act_bwd grid shaping (env knobs for tuning): pixels per lane, block cap
+static int act_ppl() {
+  static const int v = getenv("TPG_ACTB_PPL") ? atoi(getenv("TPG_ACTB_PPL")) : 4;
+  return v < 1 ? 1 : v;
+}
+static int act_cap() {
+  static const int v = getenv("TPG_ACTB_CAP") ? atoi(getenv("TPG_ACTB_CAP")) : 1024;
+  return v < 1 ? 1 : v;
+}
+
+
 static bool pix_dense_vec(const tpg_tensor& t, int h, int w, int dtype, int c) {
   const int es = dtype == TPG_BF16 ? 2 : 4, epc = 16 / es;
   if (t.dtype != dtype || t.stride[1] != 1) return false;
@@ -380,8 +445,10 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
       (act == TPG_ACT_NONE || pix_dense_vec(y, h, w, dt, c))) {
     const int64_t npix = (int64_t)n * h * w;
     const int ppi = 256 / ((c + epc - 1) / epc);
-    // >= 16 pixels per lane, <= 1024 blocks (bounds the dbias atomics per channel)
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((npix + 16 * ppi - 1) / (16 * ppi), 1024));
+    // >= 4 pixels per lane (one unrolled iteration: small maps get enough blocks to hide the
+    // load latency), <= 1024 blocks (bounds the dbias atomics per channel)
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((npix + act_ppl() * ppi - 1) / (act_ppl() * ppi),
+                                                                  act_cap()));
     const int64_t ppb = (npix + blocks - 1) / blocks;
     if (dt == TPG_BF16)
       hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
@@ -394,6 +461,15 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
     return (int)hipGetLastError();
   }
   int64_t npix = (int64_t)n * h * w;
+  if (!force_scalar && c <= 256 && pix_dense_any(gy, h, w) && pix_dense_any(g, h, w) &&
+      (act == TPG_ACT_NONE || pix_dense_any(y, h, w))) {
+    const int ppi = 256 / c;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((npix + 8 * ppi - 1) / (8 * ppi), 4 * act_cap()));
+    const int64_t ppb = (npix + blocks - 1) / blocks;
+    hipLaunchKernelGGL(act_bwd_rows_kernel, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope, gy, y, g, dbias,
+                       ppb);
+    return (int)hipGetLastError();
+  }
   int gx = (int)std::min<int64_t>((npix + 63) / 64, 2048);
   if (gx < 1) gx = 1;
   dim3 grid(gx, (c + 63) / 64);
