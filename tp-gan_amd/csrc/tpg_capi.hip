@@ -249,7 +249,8 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   else if (a.Nout <= 64) bn = 64;
   else if (a.Nout <= 96) bn = 96;
   else if (a.Nout <= 128) bn = 128;
-  else if (a.Nout <= 224) bn = a.Nout > 192 ? 224 : 128;
+  else if (a.Nout <= 208 && !getenv("TPG_HALO_NO208")) bn = a.Nout > 192 ? 208 : 128;  // (A/B hook)
+  else if (a.Nout <= 224) bn = 224;
   else bn = (cdiv(a.Nout, 224) * 224 < cdiv(a.Nout, 128) * 128) ? 224 : 128;
   const int hcap = (int)rup((int64_t)bimg * (bth + sy - 1) * (btw + sx - 1), 8);
   const int hl = std::max(3, cdiv(hcap * 4, 512));

@@ -320,9 +320,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   constexpr int RP = halo_epi_rows(BN);      // rows per pass (a whole number of wave row-blocks)
   constexpr int LDW = BN + 4;                // padded fp32 row stride
   constexpr int CG = BN / 8;                 // 8-channel groups per row
-  constexpr int IPT = RP * CG / 512;         // groups per thread per pass
+  constexpr int IPT = (RP * CG + 511) / 512;  // groups per thread per pass (the last partial)
   constexpr int NV = 8 * (int)sizeof(E) / 16;  // 16-byte vectors per group
-  static_assert(RP * CG % 512 == 0 && RP % WTM == 0, "epilogue tiling");
+  static_assert(RP % WTM == 0, "epilogue tiling");
   __syncthreads();                           // every wave is done with the halo and the ring
   int64_t* s_off = reinterpret_cast<int64_t*>(lds);           // [256][2] out / residual offsets
   float* s_bias = reinterpret_cast<float*>(lds) + 256 * 4;    // [256] bias of this block's columns
@@ -372,6 +372,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const int it = tid + 512 * k;
+        if (it >= RP * CG) continue;  // (compile-time dead unless 512 does not divide RP * CG)
         const int row = it / CG, c0 = (it - row * CG) * 8;
         const int64_t yo = s_off[2 * (pass * RP + row)];
         const int col0 = n0 + c0;
@@ -396,7 +397,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
       u32x4 rv[IPT][NV];
 #pragma unroll
       for (int k = 0; k < (R ? PF : 0); ++k) {
-        const int it = tid + 512 * k;
+        const int it = min(tid + 512 * k, RP * CG - 1);  // clamped past the last group
         const int row = it / CG, c0 = (it - row * CG) * 8;
         // unconditional (clamped) loads so that all of them issue before the first wait
         const bool ok = p.rvec && p.Nout - (n0 + c0) >= 8 && s_off[2 * (pass * RP + row)] >= 0;
@@ -407,6 +408,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const int it = tid + 512 * k;
+        if (it >= RP * CG) continue;
         const int row = it / CG, c0 = (it - row * CG) * 8;
         const int64_t yo = s_off[2 * (pass * RP + row)];
         const int col0 = n0 + c0;
@@ -452,23 +454,26 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   }
 }
 
-// {id, HL, BN, WM, WN}; id = 5 * (HL - 3) + bn index.  HL = halo chunks per thread:
+// {id, HL, BN, WM, WN}; id = 6 * (HL - 3) + bn index.  BN 208 (13 fragments on one wave
+// column) covers 193..208 output channels (the 206-channel enhance layers) without the 8 %
+// of dead MFMA columns a 224 tile carries.  HL = halo chunks per thread:
 // the halo buffer holds up to HL*128 pixels.
 #define TPG_HALO_BN(X, ID, HL)  \
   X(ID + 0, HL, 32, 8, 1)       \
   X(ID + 1, HL, 64, 8, 1)       \
   X(ID + 2, HL, 96, 8, 1)       \
   X(ID + 3, HL, 128, 4, 2)      \
-  X(ID + 4, HL, 224, 4, 2)
+  X(ID + 4, HL, 224, 4, 2)      \
+  X(ID + 5, HL, 208, 8, 1)
 #define TPG_HALO_CFGS(X)        \
   TPG_HALO_BN(X, 0, 3)          \
-  TPG_HALO_BN(X, 5, 4)          \
-  TPG_HALO_BN(X, 10, 5)
+  TPG_HALO_BN(X, 6, 4)          \
+  TPG_HALO_BN(X, 12, 5)
 
 int halo_cfg(int hl, int bn) {
-  const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : -1;
+  const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : bn == 208 ? 5 : -1;
   if (bi < 0 || hl < 3 || hl > 5) return -1;
-  return 5 * (hl - 3) + bi;
+  return 6 * (hl - 3) + bi;
 }
 
 // Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
