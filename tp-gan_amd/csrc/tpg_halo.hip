@@ -454,9 +454,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   }
 }
 
-// {id, HL, BN, WM, WN}; id = 6 * (HL - 3) + bn index.  BN 208 (13 fragments on one wave
+// {id, HL, BN, WM, WN}; id = 7 * (HL - 3) + bn index.  BN 208 (13 fragments on one wave
 // column) covers 193..208 output channels (the 206-channel enhance layers) without the 8 %
-// of dead MFMA columns a 224 tile carries.  HL = halo chunks per thread:
+// of dead MFMA columns a 224 tile carries; BN 192 tiles 384 / 576 / 768 channels exactly with
+// 24 MFMAs per wave and barrier (BN 128: 16).  HL = halo chunks per thread:
 // the halo buffer holds up to HL*128 pixels.
 #define TPG_HALO_BN(X, ID, HL)  \
   X(ID + 0, HL, 32, 8, 1)       \
@@ -464,16 +465,18 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   X(ID + 2, HL, 96, 8, 1)       \
   X(ID + 3, HL, 128, 4, 2)      \
   X(ID + 4, HL, 224, 4, 2)      \
-  X(ID + 5, HL, 208, 8, 1)
+  X(ID + 5, HL, 208, 8, 1)      \
+  X(ID + 6, HL, 192, 4, 2)
 #define TPG_HALO_CFGS(X)        \
   TPG_HALO_BN(X, 0, 3)          \
-  TPG_HALO_BN(X, 6, 4)          \
-  TPG_HALO_BN(X, 12, 5)
+  TPG_HALO_BN(X, 7, 4)          \
+  TPG_HALO_BN(X, 14, 5)
 
 int halo_cfg(int hl, int bn) {
-  const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : bn == 208 ? 5 : -1;
+  const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : bn == 208 ? 5
+               : bn == 192 ? 6 : -1;
   if (bi < 0 || hl < 3 || hl > 5) return -1;
-  return 6 * (hl - 3) + bi;
+  return 7 * (hl - 3) + bi;
 }
 
 // Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
