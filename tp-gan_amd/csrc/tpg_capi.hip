@@ -247,6 +247,7 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   int bn;
   if (a.Nout <= 32) bn = 32;
   else if (a.Nout <= 64) bn = 64;
+  else if (a.Nout <= 80 && !getenv("TPG_HALO_NO80")) bn = 80;  // (A/B hook)
   else if (a.Nout <= 96) bn = 96;
   else if (a.Nout <= 128) bn = 128;
   else if (a.Nout > 192 && a.Nout <= 208) bn = 208;

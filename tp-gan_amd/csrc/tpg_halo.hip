@@ -36,7 +36,7 @@ __device__ __forceinline__ int hswz(int row) { return ((row >> 2) & 1) << 1; }
 
 __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 128; }
 // epilogue: rows of the 256-row tile parked in LDS per pass (fp32, stride BN + 4)
-__host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 96 ? 128 : 256; }
+__host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 80 ? 128 : 256; }
 __host__ __device__ constexpr int halo_epi_lds(int bn) { return 256 * 20 + halo_epi_rows(bn) * (bn + 4) * 4; }
 
 // mask_chunk on a native 4 x u32 vector (first-class value: stays in VGPRs)
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   }
 }
 
-// {id, HL, BN, WM, WN}; id = 7 * (HL - 3) + bn index.  BN 208 (13 fragments on one wave
+// {id, HL, BN, WM, WN}; id = 8 * (HL - 3) + bn index.  BN 80 serves the 75 / 80-channel layers.  BN 208 (13 fragments on one wave
 // column) covers 193..208 output channels (the 206-channel enhance layers) without the 8 %
 // of dead MFMA columns a 224 tile carries; BN 192 tiles 384 / 576 / 768 channels exactly with
 // 24 MFMAs per wave and barrier (BN 128: 16).  HL = halo chunks per thread:
@@ -466,17 +466,18 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   X(ID + 3, HL, 128, 4, 2)      \
   X(ID + 4, HL, 224, 4, 2)      \
   X(ID + 5, HL, 208, 8, 1)      \
-  X(ID + 6, HL, 192, 4, 2)
+  X(ID + 6, HL, 192, 4, 2)      \
+  X(ID + 7, HL, 80, 8, 1)
 #define TPG_HALO_CFGS(X)        \
   TPG_HALO_BN(X, 0, 3)          \
-  TPG_HALO_BN(X, 7, 4)          \
-  TPG_HALO_BN(X, 14, 5)
+  TPG_HALO_BN(X, 8, 4)          \
+  TPG_HALO_BN(X, 16, 5)
 
 int halo_cfg(int hl, int bn) {
   const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : bn == 208 ? 5
-               : bn == 192 ? 6 : -1;
+               : bn == 192 ? 6 : bn == 80 ? 7 : -1;
   if (bi < 0 || hl < 3 || hl > 5) return -1;
-  return 7 * (hl - 3) + bi;
+  return 8 * (hl - 3) + bi;
 }
 
 // Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
