@@ -685,9 +685,17 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
 static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_tensor& g, const tpg_tensor& dw,
                         hipStream_t stream) {
   if (d->dtype != TPG_BF16 || d->stride_h != 1 || d->stride_w != 1) return 1;
-  if (d->kw != 3 && d->kw != 5 && d->kw != 7) return 1;
   const int PH = d->out_h, PW = d->out_w, QH = d->in_h, QW = d->in_w;
-  if (PW % 64 || d->pad_t >= QH || d->pad_l >= QW || !vec_ok(g, d->dtype) || !vec_ok(x, d->dtype)) return 1;
+  // row mode: one kernel row, 3/5/7 taps, 64-pixel row segments; image mode (algos 10, 11 and
+  // the default below 64 pixels of width): all taps of a 2x2 / 3x3 kernel from one halo of
+  // (64 / tw) whole rows of width tw
+  const bool row_ok = PW % 64 == 0 && (d->kw == 3 || d->kw == 5 || d->kw == 7);
+  const int tw = std::min(PW, 64);
+  const bool img_ok = d->kh == d->kw && (d->kw == 2 || d->kw == 3) && 64 % tw == 0 && PW % tw == 0 &&
+                      tw >= 8 && PH % (64 / tw) == 0 && (64 / tw + d->kh - 1) * (tw + d->kw - 1) <= 200;
+  const bool img = d->algo == 10 || d->algo == 11 || (d->algo == 0 && !row_ok);
+  if (img ? !img_ok : !row_ok) return 1;
+  if (d->pad_t >= QH || d->pad_l >= QW || !vec_ok(g, d->dtype) || !vec_ok(x, d->dtype)) return 1;
   if (g.stride[2] != (int64_t)PW * g.stride[3] || g.stride[0] != (int64_t)PH * g.stride[2]) return 1;
   if (x.stride[2] != (int64_t)QW * x.stride[3] || x.stride[0] != (int64_t)QH * x.stride[2]) return 1;
   // extents cover the last pixel's whole 16-byte chunks (vec_ok: pixel stride >= ceil8(C))
@@ -703,15 +711,18 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   a.Q = x.data; a.q_sn = (int)x.stride[0]; a.q_sh = (int)x.stride[2]; a.q_sw = (int)x.stride[3];
   a.QH = QH; a.QW = QW; a.Cb = d->in_c; a.q_bytes = (int)qb;
   a.kh = d->kh; a.kw = d->kw; a.pt = d->pad_t; a.pl = d->pad_l; a.pad_mode = d->pad_mode;
-  a.nt = d->kw == 7 ? 4 : d->kw;
+  a.nr = img ? d->kh : 1;
+  a.nt = img ? d->kw : d->kw == 7 ? 4 : d->kw;
+  a.nrg = cdiv(a.kh, a.nr);
+  a.tw = img ? tw : 64;
   // tile: fewest padded MACs, the 128 x 64 tile (best operand reuse) on ties
   int bm = 128, bc = 64;
-  if (d->algo >= 6 && d->algo <= 9) {
+  if (d->algo >= 6 && d->algo <= 11) {
     a.cfg = d->algo - 6;
     wgrad_rh_tile(a.cfg, &bm, &bc);
   } else {
     int64_t best = -1;
-    for (int c = 0; c < 4; ++c) {
+    for (int c = img ? 4 : 0; c < (img ? 6 : 4); ++c) {
       int m, b;
       wgrad_rh_tile(c, &m, &b);
       const int64_t cost = rup(a.Ca, m) * rup(a.Cb, b) * (100 + (m == 64 ? 8 : 0) + (b == 32 ? 8 : 0));
@@ -719,22 +730,23 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
     }
   }
   a.nta = cdiv(a.Ca, bm); a.ntb = cdiv(a.Cb, bc);
-  a.tiles = a.nta * a.ntb * a.kh * cdiv(a.kw, a.nt);
-  a.nkt = d->n * PH * (PW / 64);
+  a.tiles = a.nta * a.ntb * a.nrg * cdiv(a.kw, a.nt);
+  a.nkt = d->n * (PH / (64 / a.tw)) * (PW / a.tw);
   int ks = 1;
   if (d->algo >= 6 && d->ksplit >= 1) {
     ks = d->ksplit;
   } else {
     // pixel splits: whole rounds of resident blocks (one per CU, two for the <= 128-VGPR
     // tiles) against the fp32 atomics every extra split adds (~1.3 TB/s of added bytes)
-    const int resident = (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256;
-    const double flops = 2.0 * a.tiles * bm * a.nt * bc * 64.0 * a.nkt;
+    const int resident = img ? 256 : (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256;
+    const int taps = a.nr * a.nt;
+    const double flops = 2.0 * a.tiles * bm * taps * bc * 64.0 * a.nkt;
     double best = -1;
     for (int k = 1; k <= 64 && k <= a.nkt; ++k) {
       const int64_t blocks = (int64_t)a.tiles * k;
       const double rounds = (double)((blocks + resident - 1) / resident);
       const double t = rounds * flops / blocks / (4.5e12 * 256 / resident) +
-                       (k > 1 ? k * (double)a.tiles * bm * a.nt * bc * 4 / 1.3e12 : 0.0);
+                       (k > 1 ? k * (double)a.tiles * bm * taps * bc * 4 / 1.3e12 : 0.0);
       if (best < 0 || t < best) { best = t; ks = k; }
     }
   }
@@ -792,7 +804,7 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   // kernel-row halo kernel (stride-1 Conv2d, bf16, 64-pixel row segments): algo 6, and the
   // default for untuned calls when it applies
   static const bool rh_on = !getenv("TPG_WGRAD_RH") || atoi(getenv("TPG_WGRAD_RH")) != 0;  // A/B hook
-  const bool rh_algo = d->algo >= 6 && d->algo <= 9;
+  const bool rh_algo = d->algo >= 6 && d->algo <= 11;
   if (((d->algo == 0 && rh_on) || rh_algo) && !comp && !d->transposed) {
     const int rc = wgrad_rh(d, x, g, dw, (hipStream_t)stream);
     if (rc != 1) return rc;

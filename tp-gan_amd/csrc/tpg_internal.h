@@ -132,8 +132,11 @@ struct WgradRHArgs {
   const void* Q;
   int q_sn, q_sh, q_sw, QH, QW, Cb, q_bytes;
   int kh, kw, pt, pl, pad_mode;
-  int nt;                     // taps per block (3, 4, 5); groups = ceil(kw / nt)
-  int cfg;                    // tile: 0 = 128 x 64, 1 = 128 x 32, 2 = 64 x 64, 3 = 64 x 32 (a x b)
+  int nr, nt;                 // taps per block: nr kernel rows (1 = row mode, kh = image mode) x nt
+  int nrg;                    // kernel-row groups = ceil(kh / nr); tap-column groups = ceil(kw / nt)
+  int tw;                     // k-tile width (64 px = (64 / tw) rows of tw)
+  int cfg;                    // tile: 0 = 128 x 64, 1 = 128 x 32, 2 = 64 x 64, 3 = 64 x 32 (a x b);
+                              // image mode: 4 = 128 x 32, 5 = 64 x 32
   int nta, ntb, tiles;        // tiles = nta * ntb * kh * groups
   int nkt, kt_per_split, ksplit;
   float* dW;

@@ -44,23 +44,26 @@ __device__ __forceinline__ int rh_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-template <int NT, int BM, int BC>
+template <int NR, int NT, int BM, int BC>
 __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
-  constexpr int KP = 64;                     // pixels per k-tile (one image-row segment)
+  // k-tile: 64 pixels = TH x TW (TW = p.tw: a row segment of 64, or TH = 64 / TW whole rows of
+  // a narrower map); block taps: NR kernel rows x NT columns (row mode NR = 1, image mode
+  // NR = kh), all read from one (TH + NR - 1) x (TW + NT - 1) X halo of the k-tile
+  constexpr int KP = 64;
   // BM a (dY channels) x BC b (X channels) per block; GEMM columns: (tap, b)
-  constexpr int BN = NT * BC;
+  constexpr int BN = NR * NT * BC;
   constexpr int WM = (BM == 64 && BC == 64) ? 2 : 4, WN = 8 / WM;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MREP = WTM / 16, NREP = WTN / 16;
   constexpr int RBA = BM * 2, RBB = BC * 2;  // LDS row bytes
   constexpr int BYTES_A = KP * RBA;
   constexpr int GA = BYTES_A / 8192;         // 1 KiB DMA pieces per wave for dY
-  constexpr int HROWS = 72;                  // >= KP + NT - 1 halo pixels
+  constexpr int HROWS = NR == 1 ? 72 : 200;  // >= (TH + NR - 1) * (TW + NT - 1) halo pixels
   constexpr int BYTES_B = HROWS * RBB;
   constexpr int PB = (BYTES_B + 1023) / 1024, GB = (PB + 7) / 8;  // X pieces, per wave
   constexpr int RPP = 1024 / RBA, RPB = 1024 / RBB;              // rows per piece
   constexpr int STAGE = BYTES_A + GB * 8 * 1024;
-  static_assert(NT >= 3 && NT <= 5 && KP + NT - 1 <= HROWS, "taps per block");
+  static_assert(NR == 1 ? (NT >= 3 && NT <= 5) : (NR == NT && NT <= 3), "taps per block");
   static_assert(GA * 8192 == BYTES_A && GA >= 1 && GB <= 2, "dma pieces");
   static_assert(MREP * 16 * WM == BM && NREP * 16 * WN == BN, "waves");
 
@@ -75,19 +78,20 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   int t = tile;
   const int ta = t % p.nta; t /= p.nta;
   const int tb = t % p.ntb; t /= p.ntb;
-  const int r = t % p.kh;
-  const int grp = t / p.kh;
-  const int a0 = ta * BM, b0 = tb * BC, s0 = grp * NT;
+  const int r0 = (t % p.nrg) * NR;
+  const int s0 = (t / p.nrg) * NT;
+  const int a0 = ta * BM, b0 = tb * BC;
   const int kt0 = split * p.kt_per_split;
   const int nkt = min(p.nkt, kt0 + p.kt_per_split) - kt0;
   if (nkt <= 0) return;
 
   // position of k-tile kt0: (n, py, px0), advanced incrementally (all scalar)
-  const int segs = p.PW / KP;
-  int n = kt0 / (p.PH * segs);
-  int rem = kt0 - n * p.PH * segs;
-  int py = rem / segs;
-  int px0 = (rem - py * segs) * KP;
+  const int TW = p.tw, TH = KP / TW, HW = TW + NT - 1;
+  const int segs = p.PW / TW, bands = p.PH / TH;
+  int n = kt0 / (bands * segs);
+  int rem = kt0 - n * bands * segs;
+  int py = (rem / segs) * TH;
+  int px0 = (rem % segs) * TW;
 
   const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.P), 0, p.p_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Q), 0, p.q_bytes, 0x00020000);
@@ -100,16 +104,18 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   for (int j = 0; j < GA; ++j) {
     const int row = (wave * GA + j) * RPP + lane / (RBA / 16), pc = lane % (RBA / 16);
     const int c = a0 + ((pc ^ rh_swz<RBA>(row)) << 3);
-    aoff[j] = c < p.Ca ? (unsigned)((row * p.p_sw + c) * 2) : OOB;
+    aoff[j] = c < p.Ca ? (unsigned)(((row / TW) * p.p_sh + (row % TW) * p.p_sw + c) * 2) : OOB;
   }
   //   X piece j * 8 + w: halo rows (j * 8 + w) * RPB ..; pieces past PB only pad the count
-  int bhx[GB], bch[GB];
+  const int nhalo = (TH + NR - 1) * HW;
+  int bhy[GB], bhx[GB], bch[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int row = (j * 8 + wave) * RPB + lane / (RBB / 16), pc = lane % (RBB / 16);
     const int c = b0 + ((pc ^ rh_swz<RBB>(row)) << 3);
-    bhx[j] = row - p.pl + s0;                  // + px0 = X column of this halo pixel
-    bch[j] = (c < p.Cb && row < KP + NT - 1 && j * 8 + wave < PB) ? c : -1;
+    bhy[j] = row / HW + r0 - p.pt;             // + py  = X row of this halo pixel
+    bhx[j] = row % HW + s0 - p.pl;             // + px0 = X column
+    bch[j] = (c < p.Cb && row < nhalo && j * 8 + wave < PB) ? c : -1;
   }
 
   auto issue = [&](int slot, int n_, int py_, int px_) {
@@ -123,19 +129,15 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(st + (wave * GA + j) * 1024),
                                                16, vo, sbase, 0, 0);
     }
-    int qy = py_ + r - p.pt;
-    bool yok = (unsigned)qy < (unsigned)p.QH;
-    if (p.pad_mode) { qy = rh_refl(qy, p.QH); yok = true; }
-    const int qbase = (n_ * p.q_sn + qy * p.q_sh) * 2;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-      int qx = px_ + bhx[j];
-      bool ok = yok && bch[j] >= 0;
-      if (p.pad_mode) qx = rh_refl(qx, p.QW);
-      else ok = ok && (unsigned)qx < (unsigned)p.QW;
-      const unsigned off = ok ? (unsigned)((qx * p.q_sw + bch[j]) * 2) : OOB;
+      int qy = py_ + bhy[j], qx = px_ + bhx[j];
+      bool ok = bch[j] >= 0;
+      if (p.pad_mode) { qy = rh_refl(qy, p.QH); qx = rh_refl(qx, p.QW); }
+      else ok = ok && (unsigned)qy < (unsigned)p.QH && (unsigned)qx < (unsigned)p.QW;
+      const unsigned off = ok ? (unsigned)((n_ * p.q_sn + qy * p.q_sh + qx * p.q_sw + bch[j]) * 2) : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (__attribute__((address_space(3))) void*)(st + BYTES_A + (j * 8 + wave) * 1024),
-                                               16, off, yok ? qbase : 0, 0, 0);
+                                               16, off, 0, 0, 0);
     }
   };
 
@@ -151,6 +153,15 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   // Fragment reads (transposed, 4 channels x 4 pixels per lane and read): fragment r < 2*MREP
   // is dY (A), the rest X halo rows shifted by the column's tap.  Next substep's reads are
   // issued between this substep's MFMAs (as in wgrad2).
+  // halo row of this lane's pixel k = ks*32 + 8g + 4h + q for tap (0, 0): (k / TW) * HW + k % TW
+  int kbase[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = ks * 32 + 8 * g + 4 * h + q;
+      kbase[ks][h] = (k / TW) * HW + k % TW;
+    }
   auto compute = [&](int slot) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
@@ -165,7 +176,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       const int r2 = rr - 2 * MREP;
       const int col = wn * WTN + (r2 >> 1) * 16 + 4 * p4;  // (tap, b) column
       const int tap = col / BC, cb = col % BC;
-      const int row = ks * 32 + 8 * g + 4 * (r2 & 1) + q + tap;
+      const int row = kbase[ks][r2 & 1] + (tap / NT) * HW + tap % NT;
       return B + row * RBB + (((cb >> 3) ^ rh_swz<RBB>(row)) << 4) + (cb & 7) * 2;
     };
     s16x4 h[2][R];
@@ -203,8 +214,8 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   auto issue_next = [&](int slot) {
     issue(slot, in_, iy, ix);
     if (++issued < nkt) {
-      ix += KP;
-      if (ix == p.PW) { ix = 0; if (++iy == p.PH) { iy = 0; ++in_; } }
+      ix += TW;
+      if (ix == p.PW) { ix = 0; iy += TH; if (iy == p.PH) { iy = 0; ++in_; } }
     }
   };
 #define RH_WAIT_BARRIER()                                                                          \
@@ -237,8 +248,9 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
 #pragma unroll
       for (int j = 0; j < NREP; ++j) {
         const int col = wn * WTN + j * 16 + l16;
-        const int s = s0 + col / BC, b = b0 + col % BC;
-        if (s >= p.kw || b >= p.Cb) continue;
+        const int tap = col / BC;
+        const int r = r0 + tap / NT, s = s0 + tap % NT, b = b0 + col % BC;
+        if (r >= p.kh || s >= p.kw || b >= p.Cb) continue;
         float* dst = p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss;
         if (p.ksplit == 1) *dst += acc[m][j][reg];
         else atomicAdd(dst, acc[m][j][reg]);
@@ -246,12 +258,14 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
     }
 }
 
-// tile configs {id, BM, BC}; id = desc.algo - 6
+// tile configs {id, BM, BC}; id = desc.algo - 6 (ids 4, 5: image mode, 32-channel b tiles)
 #define TPG_WGRAD_RH_CFGS(X) \
   X(0, 128, 64)              \
   X(1, 128, 32)              \
   X(2, 64, 64)               \
-  X(3, 64, 32)
+  X(3, 64, 32)               \
+  X(4, 128, 32)              \
+  X(5, 64, 32)
 
 int wgrad_rh_tile(int cfg, int* bm, int* bc) {
 #define X(id, BM_, BC_) if (cfg == (id)) { *bm = BM_; *bc = BC_; return 0; }
@@ -260,11 +274,11 @@ int wgrad_rh_tile(int cfg, int* bm, int* bc) {
   return -1;
 }
 
-template <int NT, int BM, int BC>
+template <int NR, int NT, int BM, int BC>
 static int launch_rh_t(const WgradRHArgs& a, hipStream_t s) {
-  constexpr int GB = ((72 * BC * 2 + 1023) / 1024 + 7) / 8;
+  constexpr int GB = (((NR == 1 ? 72 : 200) * BC * 2 + 1023) / 1024 + 7) / 8;
   const size_t lds = 3 * (64 * BM * 2 + GB * 8 * 1024);
-  auto k = wgrad_rh_kernel<NT, BM, BC>;
+  auto k = wgrad_rh_kernel<NR, NT, BM, BC>;
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                       true);
   (void)once;
@@ -272,13 +286,23 @@ static int launch_rh_t(const WgradRHArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int launch_wgrad_rh(const WgradRHArgs& a, hipStream_t s) {
-#define X(id, BM_, BC_)                                           \
-  if (a.cfg == (id)) {                                            \
-    if (a.nt == 3) return launch_rh_t<3, BM_, BC_>(a, s);         \
-    if (a.nt == 4) return launch_rh_t<4, BM_, BC_>(a, s);         \
-    if (a.nt == 5) return launch_rh_t<5, BM_, BC_>(a, s);         \
+// row-mode configs instantiate the 1 x {3,4,5} tap groups, image-mode ones the 2x2 / 3x3
+template <int ID, int BM, int BC>
+static int launch_rh_cfg(const WgradRHArgs& a, hipStream_t s) {
+  if constexpr (ID < 4) {
+    if (a.nr == 1 && a.nt == 3) return launch_rh_t<1, 3, BM, BC>(a, s);
+    if (a.nr == 1 && a.nt == 4) return launch_rh_t<1, 4, BM, BC>(a, s);
+    if (a.nr == 1 && a.nt == 5) return launch_rh_t<1, 5, BM, BC>(a, s);
+  } else {
+    if (a.nr == 2 && a.nt == 2) return launch_rh_t<2, 2, BM, BC>(a, s);
+    if (a.nr == 3 && a.nt == 3) return launch_rh_t<3, 3, BM, BC>(a, s);
   }
+  return -1;
+}
+
+int launch_wgrad_rh(const WgradRHArgs& a, hipStream_t s) {
+#define X(id, BM_, BC_) \
+  if (a.cfg == (id)) return launch_rh_cfg<id, BM_, BC_>(a, s);
   TPG_WGRAD_RH_CFGS(X)
 #undef X
   return -1;
