@@ -690,10 +690,13 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   // the default below 64 pixels of width): all taps of a 2x2 / 3x3 kernel from one halo of
   // (64 / tw) whole rows of width tw
   const bool row_ok = PW % 64 == 0 && (d->kw == 3 || d->kw == 5 || d->kw == 7);
+  // image mode k-tile: th = floor(64 / tw) rows of tw = min(PW, 64); the fragment reads reach
+  // halo row (63 / tw + kh - 1) * (tw + kw - 1) + tw + kw - 2, inside the 200-row LDS image
   const int tw = std::min(PW, 64);
-  const bool img_ok = d->kh == d->kw && (d->kw == 2 || d->kw == 3) && 64 % tw == 0 && PW % tw == 0 &&
-                      tw >= 8 && PH % (64 / tw) == 0 && (64 / tw + d->kh - 1) * (tw + d->kw - 1) <= 200;
-  const bool img = d->algo == 10 || d->algo == 11 || (d->algo == 0 && !row_ok);
+  const bool img_ok = d->kh == d->kw && (d->kw == 2 || d->kw == 3) && PW % tw == 0 && tw >= 4 &&
+                      (63 / tw + d->kh - 1) * (tw + d->kw - 1) + tw + d->kw - 2 < 200;
+  // (untuned default only for full 64-pixel k-tiles: 40-wide maps measured slower than wgrad2)
+  const bool img = d->algo == 10 || d->algo == 11 || (d->algo == 0 && !row_ok && 64 % tw == 0);
   if (img ? !img_ok : !row_ok) return 1;
   if (d->pad_t >= QH || d->pad_l >= QW || !vec_ok(g, d->dtype) || !vec_ok(x, d->dtype)) return 1;
   if (g.stride[2] != (int64_t)PW * g.stride[3] || g.stride[0] != (int64_t)PH * g.stride[2]) return 1;
@@ -731,7 +734,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   }
   a.nta = cdiv(a.Ca, bm); a.ntb = cdiv(a.Cb, bc);
   a.tiles = a.nta * a.ntb * a.nrg * cdiv(a.kw, a.nt);
-  a.nkt = d->n * (PH / (64 / a.tw)) * (PW / a.tw);
+  a.nkt = d->n * cdiv(PH, 64 / a.tw) * (PW / a.tw);
   int ks = 1;
   if (d->algo >= 6 && d->ksplit >= 1) {
     ks = d->ksplit;

@@ -86,8 +86,10 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   if (nkt <= 0) return;
 
   // position of k-tile kt0: (n, py, px0), advanced incrementally (all scalar)
+  // TH = floor(64 / TW): pixels TH*TW..63 of a k-tile are dead (zero dY rows), and a last
+  // band may run past the map (its rows read zero as well)
   const int TW = p.tw, TH = KP / TW, HW = TW + NT - 1;
-  const int segs = p.PW / TW, bands = p.PH / TH;
+  const int segs = p.PW / TW, bands = (p.PH + TH - 1) / TH;
   int n = kt0 / (bands * segs);
   int rem = kt0 - n * bands * segs;
   int py = (rem / segs) * TH;
@@ -100,11 +102,14 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   // per-lane constants of the DMA pieces
   //   dY piece j of wave w: tile rows (GA*w + j) * RPP .. +RPP-1
   unsigned aoff[GA];
+  int ary[GA];  // pixel row of the dY tile row inside the k-tile (large = dead)
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
     const int row = (wave * GA + j) * RPP + lane / (RBA / 16), pc = lane % (RBA / 16);
     const int c = a0 + ((pc ^ rh_swz<RBA>(row)) << 3);
-    aoff[j] = c < p.Ca ? (unsigned)(((row / TW) * p.p_sh + (row % TW) * p.p_sw + c) * 2) : OOB;
+    const bool live = c < p.Ca && row < TH * TW;
+    aoff[j] = live ? (unsigned)(((row / TW) * p.p_sh + (row % TW) * p.p_sw + c) * 2) : OOB;
+    ary[j] = live ? row / TW : (1 << 28);
   }
   //   X piece j * 8 + w: halo rows (j * 8 + w) * RPB ..; pieces past PB only pad the count
   const int nhalo = (TH + NR - 1) * HW;
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
     for (int j = 0; j < GA; ++j) {
       // (a local copy: hipcc silently drops the kernel's host stub when the dependent-size
       // array element goes into the builtin directly)
-      const unsigned vo = aoff[j];
+      const unsigned vo = py_ + ary[j] < p.PH ? aoff[j] : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(st + (wave * GA + j) * 1024),
                                                16, vo, sbase, 0, 0);
     }
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
     issue(slot, in_, iy, ix);
     if (++issued < nkt) {
       ix += TW;
-      if (ix == p.PW) { ix = 0; iy += TH; if (iy == p.PH) { iy = 0; ++in_; } }
+      if (ix == p.PW) { ix = 0; iy += TH; if (iy >= p.PH) { iy = 0; ++in_; } }  // (partial last band)
     }
   };
 #define RH_WAIT_BARRIER()                                                                          \
