@@ -26,6 +26,9 @@
  *   tpg_avgpool_*           AdaptiveAvgPool2d(1) (MobileNetV2.py:173, ResNet.py:45)
  *   tpg_bn_fold             eval-mode BatchNorm2d folded into conv weights (MobileNetV2.py:100-112)
  *   tpg_bn_train_fwd/bwd    training-mode BatchNorm2d (+ fused activation) with running statistics
+ *   tpg_landmark_boxes      get_5_landmarks_pixal_position (UtilityMethods.py:148-164) + the crop
+ *                           boxes of DataAndDataset.process (DataAndDataset.py:42-54)
+ *   tpg_crop_normalize      PIL crop + ToTensor + x*2-1 (DataAndDataset.py:51-54,216-220,252-255)
  *
  * Conventions
  *   - Every tensor is described by tpg_tensor: a device pointer, a dtype and the element
@@ -209,6 +212,30 @@ int32_t tpg_bn_train_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act
                          tpg_tensor dy, tpg_tensor y, tpg_tensor x, const float* gamma,
                          const float* save_mean, const float* save_invstd, tpg_tensor dx, float* dgamma,
                          float* dbeta, float* ws, tpg_stream_t stream);
+
+/* Data path, replaces UtilityMethods.get_5_landmarks_pixal_position
+ * (UtilityMethods.py:148-164), TestDataset's landmark rescale (DataAndDataset.py:243-246) and the
+ * box arithmetic of process() (DataAndDataset.py:42-54), for n faces at once.
+ *   lm       device float[n][npts][2] landmark (x, y)
+ *   scale    device float[n][2] (sx, sy) multiplied into the 5 points after the means, or NULL
+ *   pts_idx  HOST int32[5][2] inclusive index ranges (five_pts_idx; an empty range gives NaN,
+ *            as numpy's mean of an empty slice)
+ *   patch_wh HOST int32[4][2] (width, height) of left_eye, right_eye, nose, mouth (40x40, 40x40, 40x32, 48x32)
+ *   lm5      device float[n][5][2] the five points (before the mouth midpoint)
+ *   boxes    device int32[n][4][4] (left, upper, right, lower) per patch, exactly PIL's crop box
+ *   status   device int32[n]: 0, or 1 where a point was NaN/inf (the reference raises ValueError
+ *            from math.floor there; the box row is then meaningless) */
+int32_t tpg_landmark_boxes(int32_t n, int32_t npts, const float* lm, const float* scale, const int32_t* pts_idx,
+                           const int32_t* patch_wh, float* lm5, int32_t* boxes, int32_t* status,
+                           tpg_stream_t stream);
+/* Crop + normalise u8 images into up to 8 outputs in one launch: out_k[b, c, y, x] =
+ * u/255*2-1 with u = img[b, c, upper+y, left+x], or 0 outside the image (PIL crop fill), where
+ * (left, upper) = boxes[b*box_stride + 4*slots[k] + {0, 1}], or (0, 0) when slots[k] < 0.
+ *   img_stride  HOST int64[4] element strides of the u8 image's logical (n, c, h, w) view (HWC: h*w*c, 1, w*c, c)
+ *   outs        HOST tpg_tensor[njobs] (f32 or bf16, logical NCHW), out_hw HOST int32[njobs][2] */
+int32_t tpg_crop_normalize(int32_t n, int32_t c, int32_t in_h, int32_t in_w, const uint8_t* img,
+                           const int64_t* img_stride, int32_t njobs, const tpg_tensor* outs, const int32_t* out_hw,
+                           const int32_t* slots, const int32_t* boxes, int32_t box_stride, tpg_stream_t stream);
 
 /* Library version string and the thread-local message of the last failed call. */
 const char* tpg_version(void);

@@ -85,6 +85,14 @@ EXPORTS = {
                                               ctypes.c_void_p, ctypes.c_int32]),
     "tpg_pack_prepare": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int32]),
     "tpg_pack_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p]),
+    "tpg_landmark_boxes": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_crop_normalize": (ctypes.c_int32, [ctypes.c_int32] * 4 + [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                                                   ctypes.c_int32, ctypes.POINTER(TpgTensor),
+                                                                   ctypes.POINTER(ctypes.c_int32),
+                                                                   ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p,
+                                                                   ctypes.c_int32, ctypes.c_void_p]),
     "tpg_version": (ctypes.c_char_p, []),
     "tpg_last_error": (ctypes.c_char_p, []),
 }
