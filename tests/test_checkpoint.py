@@ -1,0 +1,89 @@
+"""Checkpoint / resume: the reference's file names and formats
+(UtilityMethods.py:58-103: model_epoch_<e>.pth = state_dict, optimizer_epoch_<e>.pth =
+{optimizer, model, epoch}), with the optimizer in torch.optim.Adam's state_dict format."""
+import os
+
+import pytest
+import torch
+
+
+def _flat_with_state(seed=0):
+    import D_and_G_model as DG
+    import tpgan_train
+    torch.manual_seed(seed)
+    D = DG.Discriminator()
+    flat = tpgan_train.FlatParams(D, torch.device("cpu"))
+    g = torch.Generator().manual_seed(seed + 1)
+    flat.exp_avg.copy_(torch.randn(flat.exp_avg.shape, generator=g))
+    flat.exp_avg_sq.copy_(torch.rand(flat.exp_avg_sq.shape, generator=g))
+    flat.adam_state[0] = 7.0
+    return D, flat
+
+
+def test_optimizer_state_roundtrip_and_torch_adam():
+    D, flat = _flat_with_state()
+    sd = flat.optimizer_state_dict(1e-4, (0.5, 0.999))
+    # loads into torch.optim.Adam over the same parameters (the reference's optimizer)
+    opt = torch.optim.Adam(D.parameters(), lr=1e-4, betas=(0.5, 0.999))
+    opt.load_state_dict(sd)
+    p0 = next(D.parameters())
+    mine = flat._view(flat.exp_avg, p0, flat.offsets[0], p0.numel())
+    assert torch.equal(opt.state[p0]["exp_avg"], mine.contiguous())
+    assert float(opt.state[p0]["step"]) == 7.0
+    # and back into a FlatParams whose buffer layout is different (bucket relayout)
+    D2, flat2 = _flat_with_state(seed=3)
+    flat2.relayout(list(reversed(range(len(flat2.params)))))
+    flat2.load_optimizer_state_dict(opt.state_dict())
+    assert flat2.step == 7 and float(flat2.adam_state[0]) == 7.0
+    for i, p in enumerate(flat.params):
+        a = flat._view(flat.exp_avg_sq, p, flat.offsets[i], p.numel())
+        b = flat2._view(flat2.exp_avg_sq, flat2.params[i], flat2.offsets[i], p.numel())
+        assert torch.equal(a, b)
+
+
+def test_optimizer_state_shape_mismatch_raises():
+    D, flat = _flat_with_state()
+    sd = flat.optimizer_state_dict(1e-4)
+    sd["state"][0]["exp_avg"] = torch.zeros(3)
+    with pytest.raises(ValueError):
+        flat.load_optimizer_state_dict(sd)
+
+
+@pytest.mark.gpu
+def test_trainer_resume_matches_uninterrupted(gpu, tmp_path):
+    """Train 2 steps, checkpoint, train 1 more; a fresh trainer (other weights) that loads the
+    checkpoint and trains the same step lands on the same weights and moments."""
+    import D_and_G_model as DG
+    import tpgan_train
+    from _cases import load_det, rel
+
+    def models(seed):
+        torch.manual_seed(seed)
+        G, D = DG.Generator(64, 347, use_batchnorm=False), DG.Discriminator()
+        if seed == 0:
+            load_det(G, "G/", torch.float32)
+            load_det(D, "D/", torch.float32)
+        return G.to(gpu), D.to(gpu)
+
+    b = tpgan_train.synthetic_batch(2, gpu, seed=4)
+    G, D = models(0)
+    tr = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.float32, use_dropout=False)
+    tr.step(b)
+    tr.step(b)
+    tr.save_checkpoint(str(tmp_path), 2)
+    for tag in ("G", "D"):
+        assert os.path.exists(tmp_path / tag / "model_epoch_2.pth")
+        ck = torch.load(tmp_path / tag / "optimizer_epoch_2.pth", weights_only=True)
+        assert set(ck) == {"optimizer", "model", "epoch"} and ck["epoch"] == 2
+    tr.step(b)
+    torch.cuda.synchronize()
+    G2, D2 = models(1)
+    tr2 = tpgan_train.TPGANTrainer(G2, D2, lr=1e-4, compute_dtype=torch.float32, use_dropout=False)
+    assert tr2.load_checkpoint(str(tmp_path), 2) == 2
+    tr2.step(b)
+    torch.cuda.synchronize()
+    for f1, f2 in ((tr.fG, tr2.fG), (tr.fD, tr2.fD)):
+        assert float(f2.adam_state[0]) == 3.0
+        # same step on the same state; only the fp32 atomics order of the weight gradients differs
+        assert rel(f2.data.cpu(), f1.data.cpu()) < 1e-5
+        assert rel(f2.exp_avg.cpu(), f1.exp_avg.cpu()) < 1e-3

@@ -101,6 +101,52 @@ class FlatParams:
         self.epoch += 1
         tpgan_ops.repack(self)
 
+    # ---- checkpoint: torch.optim.Adam's state_dict format, so the files of
+    # UtilityMethods.save_optimizer (UtilityMethods.py:78-103) load into either optimizer.
+    def optimizer_state_dict(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0):
+        # the device counter advances inside graph replays: it, not self.step, is the truth
+        step = int(round(float(self.adam_state[0].item())))
+        state = {}
+        for i, p in enumerate(self.params):
+            o, n = self.offsets[i], p.numel()
+            state[i] = {"step": torch.tensor(float(step)),
+                        "exp_avg": self._view(self.exp_avg, p, o, n).detach().cpu().contiguous().clone(),
+                        "exp_avg_sq": self._view(self.exp_avg_sq, p, o, n).detach().cpu().contiguous().clone()}
+        group = {"lr": lr, "betas": tuple(betas), "eps": eps, "weight_decay": weight_decay, "amsgrad": False,
+                 "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                 "params": list(range(len(self.params)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd):
+        """Restore Adam moments and the step count (per parameter, so a checkpoint written
+        before a bucket relayout loads after it).  Missing entries mean zero moments."""
+        st = sd["state"]
+        steps = {int(round(float(v["step"]))) for v in st.values()} or {0}
+        if len(steps) != 1:
+            raise ValueError("optimizer state: parameters at different step counts %s" % sorted(steps))
+        step = steps.pop()
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for i, p in enumerate(self.params):
+                if i not in st:
+                    continue
+                o, n = self.offsets[i], p.numel()
+                for k, buf in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+                    v = st[i][k]
+                    if tuple(v.shape) != tuple(p.shape):
+                        raise ValueError("optimizer state %d/%s: shape %s, parameter %s" %
+                                         (i, k, tuple(v.shape), tuple(p.shape)))
+                    self._view(buf, p, o, n).copy_(v)
+            self.adam_state.zero_()
+            self.adam_state[0] = float(step)  # the next launch advances it and recomputes the corrections
+        self.step = step
+
+    def weights_loaded(self):
+        """After parameter values were overwritten in place (load_state_dict): rebuild the packed images."""
+        self.epoch += 1
+        tpgan_ops.repack(self)
+
 
 class GradSync:
     """Data-parallel exchange of one FlatParams: parameters broadcast from
@@ -367,6 +413,39 @@ class TPGANTrainer:
     def _phase_c(self, b):
         self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
         return {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
+
+    # ---- checkpoint / resume.  Files and formats of the reference's
+    # UtilityMethods.save_model / save_optimizer (UtilityMethods.py:58-103), one directory per
+    # network: <dir>/{G,D}/model_epoch_<e>.pth (state_dict) and optimizer_epoch_<e>.pth
+    # ({optimizer: torch.optim.Adam state_dict, model: state_dict, epoch}).  The reference
+    # writes these but never reads them back (config.py:56-57); load_checkpoint resumes.
+    def _nets(self):
+        return (("G", self.G, self.fG), ("D", self.D, self.fD))
+
+    def save_checkpoint(self, dir, epoch):
+        import os
+        torch.cuda.synchronize() if self.fG.data.is_cuda else None
+        for tag, net, flat in self._nets():
+            d = os.path.join(dir, tag)
+            os.makedirs(d, exist_ok=True)
+            sd = {k: v.detach().cpu().contiguous().clone() for k, v in net.state_dict().items()}
+            torch.save(sd, os.path.join(d, "model_epoch_%s.pth" % epoch))
+            torch.save({"optimizer": flat.optimizer_state_dict(self.lr, self.betas), "model": sd, "epoch": epoch},
+                       os.path.join(d, "optimizer_epoch_%s.pth" % epoch))
+
+    def load_checkpoint(self, dir, epoch):
+        """Restore both networks and their Adam states; returns the stored epoch.  Loaded with
+        weights_only=True (nothing in the file is executed)."""
+        import os
+        out = None
+        for tag, net, flat in self._nets():
+            ck = torch.load(os.path.join(dir, tag, "optimizer_epoch_%s.pth" % epoch), map_location="cpu",
+                            weights_only=True)
+            net.load_state_dict(ck["model"])  # copies into the flat-buffer views
+            flat.load_optimizer_state_dict(ck["optimizer"])
+            flat.weights_loaded()
+            out = ck["epoch"]
+        return out  # every rank reads the same files: replicas stay identical without a broadcast
 
     def step(self, b):
         """One eager G+D train step."""
