@@ -237,6 +237,14 @@ int32_t tpg_crop_normalize(int32_t n, int32_t c, int32_t in_h, int32_t in_w, con
                            const int64_t* img_stride, int32_t njobs, const tpg_tensor* outs, const int32_t* out_hw,
                            const int32_t* slots, const int32_t* boxes, int32_t box_stride, tpg_stream_t stream);
 
+/* Deterministic mode (process-wide, off by default; SURVEY.md §5 race detection): every
+ * reduction runs in a fixed order — no split-K fp32 atomics in the conv forward / input
+ * gradient, weight gradients with one pixel split (each dW element added once), bias
+ * gradients summed by one block — so two runs on the same inputs are bit-identical.  Slower;
+ * meant for parity and run-to-run tests. */
+void tpg_set_deterministic(int32_t on);
+int32_t tpg_get_deterministic(void);
+
 /* Library version string and the thread-local message of the last failed call. */
 const char* tpg_version(void);
 const char* tpg_last_error(void);

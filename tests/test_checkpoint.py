@@ -87,3 +87,89 @@ def test_trainer_resume_matches_uninterrupted(gpu, tmp_path):
         # same step on the same state; only the fp32 atomics order of the weight gradients differs
         assert rel(f2.data.cpu(), f1.data.cpu()) < 1e-5
         assert rel(f2.exp_avg.cpu(), f1.exp_avg.cpu()) < 1e-3
+
+
+class _Tiny(torch.nn.Module):
+    def __init__(self, a, b):
+        super(_Tiny, self).__init__()
+        self.lin = torch.nn.Linear(a, b)
+        self.conv = torch.nn.Conv2d(b, 2, 3)
+
+
+def _tiny_trainer(seed, **kw):
+    import tpgan_train
+    torch.manual_seed(seed)
+    tr = tpgan_train.TPGANTrainer(_Tiny(4, 6), _Tiny(3, 5), lr=1e-4, compute_dtype=torch.float32, **kw)
+    for f in (tr.fG, tr.fD):
+        g = torch.Generator().manual_seed(seed + 7)
+        f.exp_avg.copy_(torch.randn(f.exp_avg.shape, generator=g))
+        f.exp_avg_sq.copy_(torch.rand(f.exp_avg_sq.shape, generator=g))
+        f.adam_state[0] = 5.0
+    return tr
+
+
+def _ckpt_worker(rank, world, port, path, q):
+    import socket  # noqa: F401
+    import sys
+    import torch.distributed as dist
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "tp-gan_amd"), os.path.join(repo, "tests")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from test_checkpoint import _tiny_trainer
+        tr = _tiny_trainer(rank)       # broadcast: both ranks hold rank 0's weights
+        if rank == 1:                  # rank-local state that must NOT reach the files
+            tr.fG.exp_avg.fill_(123.0)
+        saved = [t.clone() for t in (tr.fG.data, tr.fD.data)]
+        tr.save_checkpoint(path, 3)
+        files = sorted(os.listdir(os.path.join(path, "G")))
+        tr2 = _tiny_trainer(10 + rank)
+        ep = tr2.load_checkpoint(path, 3)
+        ok = ep == 3 and torch.equal(tr2.fG.data, saved[0]) and torch.equal(tr2.fD.data, saved[1])
+        ok_m = not bool((tr2.fG.exp_avg == 123.0).any())  # rank 0 wrote its own moments
+        q.put((rank, ok, ok_m, files))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_checkpoint_world2_rank0_writes_atomically(tmp_path):
+    """under torchrun every rank used to torch.save the same paths at once.  Now
+    rank 0 writes each file under a temporary name and renames it into place, all ranks
+    meet at a barrier, and every rank then loads the same complete files (gloo, CPU)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=280) for _ in range(2))
+    for p in procs:
+        p.join(60)
+    for rank, ok, ok_m, files in res:
+        assert ok and ok_m, rank
+        assert files == ["model_epoch_3.pth", "optimizer_epoch_3.pth"], files  # no temporaries left
+
+
+def test_checkpoint_hparam_mismatch(tmp_path):
+    """a file written with other Adam hyperparameters (the reference's getOptimizer
+    uses betas (0.9, 0.999)) raises instead of silently resuming with the trainer's betas;
+    adopt_hparams=True takes the stored lr / betas instead."""
+    tr = _tiny_trainer(0)
+    tr.betas = (0.9, 0.999)
+    tr.lr = 3e-4
+    tr.save_checkpoint(str(tmp_path), 1)
+    tr2 = _tiny_trainer(1)  # betas (0.5, 0.999), lr 1e-4
+    with pytest.raises(ValueError, match="betas"):
+        tr2.load_checkpoint(str(tmp_path), 1)
+    tr3 = _tiny_trainer(2)
+    assert tr3.load_checkpoint(str(tmp_path), 1, adopt_hparams=True) == 1
+    assert tr3.betas == (0.9, 0.999) and tr3.lr == 3e-4
+    assert torch.equal(tr3.fG.data, tr.fG.data)

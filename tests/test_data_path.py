@@ -172,3 +172,23 @@ def test_gpu_empty_batch(gpu):
     fb = DD.FaceBatcher(gpu)
     out = fb(torch.zeros(0, 128, 128, 3, dtype=torch.uint8, device=gpu), torch.zeros(0, 68, 2, device=gpu))
     assert out["left_eye"].shape == (0, 3, 40, 40)
+
+
+@pytest.mark.gpu
+def test_gpu_face_batcher_rejects_host_tensors(gpu):
+    """Raw pointers go to the kernels: CPU inputs (TrainDataset(raw=True), numpy) must raise,
+    not hand the GPU a host address."""
+    import DataAndDataset as DD
+    fb = DD.FaceBatcher(gpu)
+    img = torch.zeros(2, 128, 128, 3, dtype=torch.uint8)
+    lm = torch.full((2, 68, 2), 64.0)
+    with pytest.raises(ValueError, match="must be on"):
+        fb(img, lm.to(gpu))
+    with pytest.raises(ValueError, match="must be on"):
+        fb(img.to(gpu), lm)
+    with pytest.raises(ValueError, match="must be on"):
+        fb.landmark_boxes(lm.to(gpu), torch.ones(2, 2))
+    with pytest.raises(ValueError, match="must be on"):
+        fb.normalize(img)
+    out = DD.FaceBatcher("cuda")(img.to(gpu), lm.to(gpu))  # "cuda" means the current device
+    assert out["I128"].device == gpu

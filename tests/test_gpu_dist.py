@@ -78,3 +78,136 @@ def test_dp_overlap_two_ranks_one_gpu(gpu):
     assert nb0 == nb1 and nb0 > 10 and l0 and l1
     assert off0 == off1
     assert max(e0) > 0 and max(e1) > 0  # some buckets went out while the backward was running
+
+
+LR_EQ = 1e-4  # the bench's learning rate
+
+
+def _moments(tr):
+    """Adam first / second moments per parameter, read through each parameter's own offset
+    (layout-independent: a relayout that permuted them would show here)."""
+    out = []
+    for f in (tr.fG, tr.fD):
+        for buf in (f.exp_avg, f.exp_avg_sq):
+            out.append([f._view(buf, p, f.offsets[i], p.numel()).detach().clone() for i, p in enumerate(f.params)])
+    return out
+
+
+def _copy_state(dst, src):
+    """dst's parameters, Adam moments and step counters := src's, per parameter (the two
+    flat layouts differ once src has relaid out its buckets)."""
+    with torch.no_grad():
+        for fd, fs in ((dst.fG, src.fG), (dst.fD, src.fD)):
+            for i, (pd, ps) in enumerate(zip(fd.params, fs.params)):
+                pd.data.copy_(ps.data)
+                for bd, bs in ((fd.exp_avg, fs.exp_avg), (fd.exp_avg_sq, fs.exp_avg_sq)):
+                    fd._view(bd, pd, fd.offsets[i], pd.numel()).copy_(fs._view(bs, ps, fs.offsets[i], ps.numel()))
+            fd.adam_state.copy_(fs.adam_state)
+            fd.step = fs.step
+            fd.weights_loaded()
+
+
+def _equiv_worker(rank, world, port, q):
+    """Rank 0 also runs the single-process reference (B = 4) in a one-rank group; both ranks
+    run the DP step on their half of the same batch.  Before the second step the reference
+    takes the DP run's state, so step 2 starts from the same point on both sides.  fp32 MFMA
+    path, deterministic reductions."""
+    sys.path[:0] = [REPO, os.path.join(REPO, "tp-gan_amd"), os.path.join(REPO, "tests")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import D_and_G_model as DG
+        import tpgan_ops
+        import tpgan_train
+        from _cases import load_det, rel
+        dev = torch.device("cuda", 0)
+        solo = dist.new_group([0])
+
+        def models():
+            G = DG.Generator(64, 347, use_batchnorm=False)
+            D = DG.Discriminator()
+            load_det(G, "G/", torch.float32)
+            load_det(D, "D/", torch.float32)
+            return G.to(dev), D.to(dev)
+
+        def snap(tr, G, D, loss, scale):
+            return ([p.grad.detach().clone() / scale for p in G.parameters()],
+                    [p.grad.detach().clone() / scale for p in D.parameters()],
+                    [p.detach().clone() for p in G.parameters()],
+                    [p.detach().clone() for p in D.parameters()], loss, _moments(tr))
+
+        full = [tpgan_train.synthetic_batch(4, dev, seed=300 + s) for s in range(2)]
+        res, ref, got = {}, [], []
+        with tpgan_ops.deterministic():
+            G2, D2 = models()
+            t2 = tpgan_train.TPGANTrainer(G2, D2, lr=LR_EQ, compute_dtype=torch.float32, use_dropout=False,
+                                          bucket_mb=16.0)
+            if rank == 0:
+                G1, D1 = models()
+                t1 = tpgan_train.TPGANTrainer(G1, D1, lr=LR_EQ, compute_dtype=torch.float32, use_dropout=False,
+                                              process_group=solo)
+            for s, b in enumerate(full):
+                if rank == 0:  # the 1-GPU run at global batch 4
+                    if s:
+                        _copy_state(t1, t2)
+                    out = t1.step(b)
+                    torch.cuda.synchronize()
+                    ref.append(snap(t1, G1, D1, float(out["loss_G"]), 1))
+                dist.barrier()
+                half = {k: v[2 * rank:2 * rank + 2] for k, v in b.items()}
+                out = t2.step(half)
+                torch.cuda.synchronize()
+                lg = torch.tensor([float(out["loss_G"])], dtype=torch.float64)
+                dist.all_reduce(lg)  # the 1-GPU loss is the mean of the two half-batch means
+                got.append(snap(t2, G2, D2, float(lg) / world, world))
+            res["relayout"] = bool(t2.gsync.order_learned)
+        if rank == 0:
+            cat = lambda ts: torch.cat([t.double().reshape(-1) for t in ts]).cpu()  # noqa: E731
+            for s, ((gG, gD, pG, pD, lG, mo1), (hG, hD, qG, qD, mG, mo2)) in enumerate(zip(ref, got)):
+                res["step%d" % s] = {
+                    "loss": abs(lG - mG) / abs(lG),
+                    "gradG": rel(cat(hG), cat(gG)), "gradD": rel(cat(hD), cat(gD)),
+                    "paramG": rel(cat(qG), cat(pG)), "paramD": rel(cat(qD), cat(pD)),
+                    "moments": max(rel(cat(b), cat(a)) for a, b in zip(mo1, mo2))}
+        q.put((rank, res))
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_dp_equals_single_gpu_at_global_batch(gpu):
+    """after a full step, 2 ranks x B = 2 equal one process at B = 4 (fp32,
+    deterministic mode): the all-reduced gradients (averaged), the updated parameters and the
+    loss; then a second step, run on the learned bucket layout (the post-step-1 relayout
+    moves parameters, gradients and Adam moments) from the DP run's state copied into the
+    1-GPU trainer, matches the same way (Adam moments compared per parameter).  A rank-symmetric bug
+    (wrong grad_scale, a bucket skipped on both ranks, moments permuted by the relayout)
+    breaks the equality, which replica-equality alone cannot see.  Deterministic mode sums each
+    sample's conv outputs in one order whatever the batch size, so only the weight-gradient sums
+    regroup (2 images per rank + the all-reduce instead of 4): measured ~7e-7 on the gradients,
+    bound 1e-5; loss bound 1e-6.  A skipped bucket or a wrong scale is O(1)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_equiv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=380) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    r0 = res[0]
+    assert isinstance(r0, dict), r0
+    assert r0["relayout"]
+    for s in ("step0", "step1"):
+        m = r0[s]
+        assert m["loss"] < 1e-6, (s, m)
+        assert m["moments"] < 1e-5, (s, m)
+        assert m["gradG"] < 1e-5 and m["gradD"] < 1e-5, (s, m, r0["worstG" + s[-1]])
+        # parameters: Adam's first steps normalise every element (g / (|g| + eps)), so an
+        # element whose gradient is itself at the 1e-7 floor moves by up to ~lr either way
+        assert m["paramG"] < 1e-5 and m["paramD"] < 1e-5, (s, m)

@@ -95,13 +95,15 @@ def test_train_step_vs_oracle(gpu):
     """One fp32 trainer step (G forward, D-step + HIP Adam, G-step through the updated D
     + HIP Adam) against the oracle: losses, flat gradients (global-norm 1e-3) and the
     updated parameters."""
+    import tpgan_ops
     import tpgan_train
     from oracle import tpgan_oracle as O
     G, D = _models(gpu)
     tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.float32, use_dropout=False)
     b = _batch(2)
-    out = tr.step({k: (v.float() if v.is_floating_point() else v).to(gpu) for k, v in b.items()})
-    torch.cuda.synchronize()
+    with tpgan_ops.deterministic():  # fixed-order reductions: no run-to-run kink flips
+        out = tr.step({k: (v.float() if v.is_floating_point() else v).to(gpu) for k, v in b.items()})
+        torch.cuda.synchronize()
     PG, PD = O.make_params(torch.float64)
     P0 = {("G", k): v.clone() for k, v in PG.items()}
     P0.update({("D", k): v.clone() for k, v in PD.items()})
@@ -118,11 +120,10 @@ def test_train_step_vs_oracle(gpu):
         mine = torch.cat([p.grad.detach().double().cpu().reshape(-1) for p in model.parameters()])
         ref = torch.cat([gr.detach().reshape(-1) for gr in grads])
         floor = rel(torch.cat([gr.detach().double().reshape(-1) for gr in grads32]), ref)
-        # <= 1e-2 per tensor.  Globally 2e-3 rather than 1e-3: in about half
-        # of the runs one LeakyReLU pre-activation of D.model.3 (stride-2 conv, split-K
-        # forward summed with fp32 atomics) lands within 1e-7 of zero on the other side,
-        # which moves D's concatenated gradient by 1.27e-3 (model.3.0.bias by 3.8e-3).
-        assert rel(mine, ref) < max(2e-3, 3 * floor), (tag, rel(mine, ref), floor)
+        # global 1e-3, <= 1e-2 per tensor.  Deterministic mode: with split-K
+        # fp32 atomics a D.model.3 LeakyReLU pre-activation within 1e-7 of zero used to land on
+        # either side from run to run (round 1 had to widen this bound to 2e-3).
+        assert rel(mine, ref) < max(1e-3, 3 * floor), (tag, rel(mine, ref), floor)
         for (k, p), gr in zip(model.named_parameters(), grads):
             if float(gr.norm()) > 0:
                 assert rel(p.grad.detach().cpu(), gr) < 1e-2, (tag, k)
@@ -142,6 +143,8 @@ def _restore(tr, snap):
     ts = [t for f in (tr.fG, tr.fD) for t in (f.data, f.exp_avg, f.exp_avg_sq, f.adam_state)]
     for t, s in zip(ts, snap):
         t.copy_(s)
+    for f in (tr.fG, tr.fD):  # the pre-packed bf16 weight images follow the restored values
+        f.weights_loaded()
 
 
 @pytest.mark.parametrize("segmented", [False, True])
@@ -260,3 +263,59 @@ def test_prepacked_weights_match_inline_packing(gpu):
     for i in range(3):
         floor = rel(a2[i].cpu(), a[i].cpu())
         assert rel(c[i].cpu(), a[i].cpu()) <= max(3 * floor, 1e-6), (i, rel(c[i].cpu(), a[i].cpu()), floor)
+
+
+def test_deterministic_mode_bit_identical(gpu):
+    """tpg_set_deterministic: two bf16 train steps from the same state give bit-identical
+    parameters, gradients and Adam moments (SURVEY.md §5 race detection / run-to-run)."""
+    import tpgan_ops
+    import tpgan_train
+    G, D = _models(gpu)
+    tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False)
+    b = tpgan_train.synthetic_batch(4, gpu, seed=17)
+    with tpgan_ops.deterministic():
+        tr.step(b)
+        torch.cuda.synchronize()
+        snap = _snapshot(tr)
+        res = []
+        for _ in range(2):
+            _restore(tr, snap)
+            tr.step(b)
+            torch.cuda.synchronize()
+            res.append([t.clone() for t in (tr.fG.data, tr.fD.data, tr.fG.grad, tr.fD.grad, tr.fG.exp_avg_sq)])
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
+
+
+def test_bs32_step_properties(gpu):
+    """The benchmark's configuration (bf16, bs32, flat params, autotuned kernels) against the
+    same step in fp32 (deterministic) from the same weights and batch: losses finite and within
+    2e-2, parameters finite, G / D gradients within a bound scaled from B=2.  Why scaled: the
+    batch-mean gradient shrinks as per-sample contributions cancel (G: |g| at bs32 is ~1/4 of
+    B=2), while the error of bf16 weights and activations is largely systematic (the same
+    rounded weights for every sample) and does not; so bs32 may sit at
+    err(B=2) * |g(B=2)| / |g(bs32)|, and the test allows 3x that (never below 5e-2)."""
+    import tpgan_ops
+    import tpgan_train
+    res = {}
+    for B in (2, 32):
+        for dt in (torch.float32, torch.bfloat16):
+            G, D = _models(gpu)
+            tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=dt, use_dropout=False)
+            b = tpgan_train.synthetic_batch(B, gpu, seed=23)
+            with tpgan_ops.deterministic(dt == torch.float32):
+                out = tr.step(b)
+                torch.cuda.synchronize()
+            assert np.isfinite(float(out["loss_D"])) and np.isfinite(float(out["loss_G"])), (B, dt)
+            for f in (tr.fG, tr.fD):
+                assert bool(torch.isfinite(f.grad).all()) and bool(torch.isfinite(f.data).all()), (B, dt)
+            res[(B, dt)] = (float(out["loss_D"]), float(out["loss_G"]), tr.fG.grad.cpu(), tr.fD.grad.cpu())
+            del tr, G, D
+            torch.cuda.empty_cache()
+    a, c = res[(32, torch.float32)], res[(32, torch.bfloat16)]
+    assert abs(c[0] - a[0]) <= 2e-2 * max(abs(a[0]), 1e-2) and abs(c[1] - a[1]) <= 2e-2 * abs(a[1]), (a[:2], c[:2])
+    a2, c2 = res[(2, torch.float32)], res[(2, torch.bfloat16)]
+    for i, tag in ((2, "G"), (3, "D")):
+        err2, err32 = rel(c2[i], a2[i]), rel(c[i], a[i])
+        shrink = float(a2[i].norm()) / float(a[i].norm())
+        assert err32 < max(5e-2, 3 * err2 * shrink), (tag, err32, err2, shrink)

@@ -11,6 +11,8 @@ import collections
 import csv
 import re
 
+BY_GRID = False
+
 
 def short(name):
     name = re.sub(r"\(tpg::\w+\)$", "", name)
@@ -22,7 +24,11 @@ def load(path):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            name = r["Kernel_Name"]
+            if BY_GRID:
+                name = short(name)[:60] + " g%sx%sx%s" % (r.get("Grid_Size_X", "?"), r.get("Grid_Size_Y", "?"),
+                                                        r.get("Grid_Size_Z", "?"))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
     return rows
 
@@ -41,7 +47,10 @@ def main():
     ap.add_argument("--csv")
     ap.add_argument("--steps", type=int, default=0)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--by-grid", action="store_true", help="group by (kernel, grid size): one line per layer shape")
     a = ap.parse_args()
+    global BY_GRID
+    BY_GRID = a.by_grid
     rows, steps = window(load(a.trace), a.steps)
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 1e30])
     for t0, t1, name in rows:

@@ -196,15 +196,26 @@ class FaceBatcher:
     def __init__(self, device, dtype=torch.float32, pts_idx=FIVE_PTS_IDX_REPAIRED, check=True):
         self.lib = L.load()
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.dtype = dtype
         self.check = check
         self._idx = (ctypes.c_int32 * 10)(*[v for r in pts_idx for v in r])
         self._wh = (ctypes.c_int32 * 8)(*[v for n in PATCH_NAMES for v in PATCH_SIZE[n]])
 
+    def _on_device(self, t, name):
+        """The kernels take raw pointers: a tensor on another device (e.g. the CPU output of
+        TrainDataset(raw=True) or numpy) would hand them a host address."""
+        if t.device != self.device:
+            raise ValueError("%s must be on %s (FaceBatcher's device), got %s" % (name, self.device, t.device))
+
     def landmark_boxes(self, lm68, scale=None):
         """-> (lm5 float32 [B, 5, 2], boxes int32 [B, 4, 4] (left, upper, right, lower), status int32 [B])."""
         if lm68.dtype != torch.float32 or lm68.dim() != 3 or lm68.shape[2] != 2:
             raise ValueError("lm68 must be float32 [B, npts, 2]")
+        self._on_device(lm68, "lm68")
+        if scale is not None:
+            self._on_device(scale, "scale")
         lm68 = lm68.contiguous()
         B = lm68.shape[0]
         lm5 = torch.empty(B, 5, 2, dtype=torch.float32, device=self.device)
@@ -214,14 +225,16 @@ class FaceBatcher:
             if scale.dtype != torch.float32 or tuple(scale.shape) != (B, 2):
                 raise ValueError("scale must be float32 [B, 2]")
             scale = scale.contiguous()
-        L.check(self.lib.tpg_landmark_boxes(B, lm68.shape[1], lm68.data_ptr(),
-                                            scale.data_ptr() if scale is not None else None, self._idx, self._wh,
-                                            lm5.data_ptr(), boxes.data_ptr(), status.data_ptr(), L.stream_ptr()))
+        with torch.cuda.device(self.device):  # the launch goes to this device's current stream
+            L.check(self.lib.tpg_landmark_boxes(B, lm68.shape[1], lm68.data_ptr(),
+                                                scale.data_ptr() if scale is not None else None, self._idx, self._wh,
+                                                lm5.data_ptr(), boxes.data_ptr(), status.data_ptr(), L.stream_ptr()))
         return lm5, boxes, status
 
     def _crop(self, img_u8, jobs, boxes):
         if img_u8.dtype != torch.uint8 or img_u8.dim() != 4:
             raise ValueError("img_u8 must be uint8 [B, H, W, C]")
+        self._on_device(img_u8, "img_u8")
         B, H, W, C = img_u8.shape
         s = img_u8.stride()
         strides = (ctypes.c_int64 * 4)(s[0], s[3], s[1], s[2])  # logical (n, c, h, w)
@@ -232,8 +245,9 @@ class FaceBatcher:
             res[name] = t
             outs[k] = L.tt(t)
             hw[2 * k], hw[2 * k + 1], slots[k] = h, w, slot
-        L.check(self.lib.tpg_crop_normalize(B, C, H, W, img_u8.data_ptr(), strides, len(jobs), outs, hw, slots,
-                                            boxes.data_ptr() if boxes is not None else None, 16, L.stream_ptr()))
+        with torch.cuda.device(self.device):
+            L.check(self.lib.tpg_crop_normalize(B, C, H, W, img_u8.data_ptr(), strides, len(jobs), outs, hw, slots,
+                                                boxes.data_ptr() if boxes is not None else None, 16, L.stream_ptr()))
         return res
 
     def normalize(self, img_u8, name="I128"):

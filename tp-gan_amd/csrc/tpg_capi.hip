@@ -41,6 +41,9 @@ int launch_reflect_fold(int N, int C, int H, int W, int pt, int pb, int pl, int 
 using namespace tpg;
 
 static thread_local std::string g_err;
+static int g_det = 0;  // tpg_set_deterministic
+
+int tpg::deterministic() { return __atomic_load_n(&g_det, __ATOMIC_RELAXED); }
 
 static int32_t fail(int32_t code, const char* fmt, ...) {
   char buf[512];
@@ -104,7 +107,7 @@ static void finish(Prob& P, int dtype, int M) {
   const int blocks = cdiv(M, bm) * (npad / bn);
   a.ksplit = 1;
   a.kt_per_split = std::max(nkt, 1);
-  if (blocks < 480 && nkt >= 8) {
+  if (blocks < 480 && nkt >= 8 && !deterministic()) {
     int ks = std::min(cdiv(960, blocks), nkt / 4);
     if (ks > 1) {
       a.kt_per_split = cdiv(nkt, ks);
@@ -290,7 +293,9 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   static const int split_below = getenv("TPG_SPLIT_BELOW") ? atoi(getenv("TPG_SPLIT_BELOW")) : 256;  // tuning
   static const int split_to = getenv("TPG_SPLIT_TO") ? atoi(getenv("TPG_SPLIT_TO")) : 256;
   static const int split_steps = getenv("TPG_SPLIT_STEPS") ? atoi(getenv("TPG_SPLIT_STEPS")) : 4;
-  if (base < split_below) {
+  // (deterministic mode: no k-split at all, so a sample's outputs are summed in the same
+  // order whatever the batch size — the DP run then matches the 1-GPU run at its global batch)
+  if (base < split_below && !deterministic()) {
     const int kps_min = cdiv(split_steps, a.ntaps);
     ks = (int)std::min<int64_t>(cdiv(split_to, (int)base), std::max(1, h.nks / kps_min));
   }
@@ -754,6 +759,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
     }
   }
   ks = std::max(1, std::min(ks, a.nkt));
+  if (deterministic()) ks = 1;  // one block adds each dW element once
   a.kt_per_split = cdiv(a.nkt, ks);
   a.ksplit = cdiv(a.nkt, a.kt_per_split);
   a.dW = reinterpret_cast<float*>(dw.data);
@@ -848,6 +854,7 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
         bm = fm; bn = fn; bks = std::min(fk, nkt);
       }
     }
+    if (deterministic()) bks = 1;
     a.pix_per_split = (int)rup(cdiv(a.npix, bks), kp);
     a.ksplit = cdiv(a.npix, a.pix_per_split);
     const int es = esize(d->dtype);
@@ -877,6 +884,7 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   const int tiles = cdiv(a.Ca, bm) * cdiv(a.Cb, bn) * a.ntaps;
   int ks = std::max(1, cdiv(1536, tiles));
   ks = std::min(ks, std::max(1, a.npix / (32 * 16)));
+  if (deterministic()) ks = 1;
   a.pix_per_split = (int)rup(cdiv(a.npix, ks), 32);
   a.ksplit = cdiv(a.npix, a.pix_per_split);
   return hip_check(launch_wgrad(a, d->dtype, cfg, (hipStream_t)stream), "wgrad");
@@ -933,6 +941,9 @@ extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, floa
   if (rc == -1) return fail(-15, "adam: buffers must be 16-byte aligned");
   return hip_check(rc, "adam");
 }
+
+extern "C" void tpg_set_deterministic(int32_t on) { __atomic_store_n(&g_det, on ? 1 : 0, __ATOMIC_RELAXED); }
+extern "C" int32_t tpg_get_deterministic(void) { return tpg::deterministic(); }
 
 extern "C" const char* tpg_version(void) { return "tpgan_hip 0.1 gfx950"; }
 extern "C" const char* tpg_last_error(void) { return g_err.c_str(); }

@@ -447,8 +447,10 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
     const int ppi = 256 / ((c + epc - 1) / epc);
     // >= 4 pixels per lane (one unrolled iteration: small maps get enough blocks to hide the
     // load latency), <= 1024 blocks (bounds the dbias atomics per channel)
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((npix + act_ppl() * ppi - 1) / (act_ppl() * ppi),
-                                                                  act_cap()));
+    // deterministic mode with a bias gradient: one block, so every dbias element gets ONE
+    // atomic add (a fixed-order sum)
+    const int64_t blocks = (dbias && deterministic()) ? 1 :
+        std::max<int64_t>(1, std::min<int64_t>((npix + act_ppl() * ppi - 1) / (act_ppl() * ppi), act_cap()));
     const int64_t ppb = (npix + blocks - 1) / blocks;
     if (dt == TPG_BF16)
       hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
@@ -464,14 +466,15 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
   if (!force_scalar && c <= 256 && pix_dense_any(gy, h, w) && pix_dense_any(g, h, w) &&
       (act == TPG_ACT_NONE || pix_dense_any(y, h, w))) {
     const int ppi = 256 / c;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((npix + 8 * ppi - 1) / (8 * ppi), 4 * act_cap()));
+    const int64_t blocks = (dbias && deterministic()) ? 1 :
+        std::max<int64_t>(1, std::min<int64_t>((npix + 8 * ppi - 1) / (8 * ppi), 4 * act_cap()));
     const int64_t ppb = (npix + blocks - 1) / blocks;
     hipLaunchKernelGGL(act_bwd_rows_kernel, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope, gy, y, g, dbias,
                        ppb);
     return (int)hipGetLastError();
   }
   int gx = (int)std::min<int64_t>((npix + 63) / 64, 2048);
-  if (gx < 1) gx = 1;
+  if (gx < 1 || (dbias && deterministic())) gx = 1;
   dim3 grid(gx, (c + 63) / 64);
   hipLaunchKernelGGL(act_bwd_kernel, grid, dim3(256), 0, s, n, c, h, w, act, slope, gy, y, g, dbias);
   return (int)hipGetLastError();
@@ -522,9 +525,10 @@ extern "C" int32_t tpg_maxout_bwd_impl(int32_t b, int32_t m, tpg_tensor gy, cons
 extern "C" int32_t tpg_adam_impl(int64_t numel, float* param, const float* grad, float* m, float* v, float lr,
                                   float b1, float b2, float eps, float wd, int32_t host_step, float gscale,
                                   float* state, hipStream_t s) {
-  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, state, b1, b2, host_step);
+  // argument checks before any launch: an error must not advance the device step counter
   const bool vec = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
   if (!vec) return -1;
+  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, state, b1, b2, host_step);
   int blocks = (int)std::min<int64_t>((numel / 4 + 255) / 256, 4096);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, state,

@@ -300,6 +300,10 @@ struct HaloArgs {
 // sets the thread-local message returned by tpg_last_error() (tpg_capi.hip); returns code
 int record_error(int code, const char* msg);
 
+// tpg_set_deterministic(): every reduction in a fixed order (no split-K / pixel-split fp32
+// atomics, one block per bias-gradient sum); process-wide, for parity and run-to-run tests
+int deterministic();
+
 // launchers (return hipError_t as int); cfg selects the tile shape
 int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s);
 int igemm_cfg_bn(int cfg);

@@ -93,6 +93,8 @@ EXPORTS = {
                                                                    ctypes.POINTER(ctypes.c_int32),
                                                                    ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p,
                                                                    ctypes.c_int32, ctypes.c_void_p]),
+    "tpg_set_deterministic": (None, [ctypes.c_int32]),
+    "tpg_get_deterministic": (ctypes.c_int32, []),
     "tpg_version": (ctypes.c_char_p, []),
     "tpg_last_error": (ctypes.c_char_p, []),
 }

@@ -12,6 +12,7 @@ Master weights and their gradients stay float32.
 """
 import contextlib
 import ctypes
+import os
 
 import torch
 
@@ -78,8 +79,21 @@ def get_compute_dtype():
     return _DTYPE[-1]
 
 
+@contextlib.contextmanager
+def deterministic(on=True):
+    """Fixed-order reductions in every HIP op inside the block (tpg_set_deterministic):
+    bit-identical reruns, for parity tests; slower."""
+    lib = load()
+    prev = lib.tpg_get_deterministic()
+    lib.tpg_set_deterministic(1 if on else 0)
+    try:
+        yield
+    finally:
+        lib.tpg_set_deterministic(prev)
+
+
 # Run the Generator's four local pathways on side streams (D_and_G_model.Generator).
-MULTISTREAM = True
+MULTISTREAM = os.environ.get("TPG_MULTISTREAM", "1") != "0"
 _SIDE = {}
 
 

@@ -119,7 +119,9 @@ class FlatParams:
 
     def load_optimizer_state_dict(self, sd):
         """Restore Adam moments and the step count (per parameter, so a checkpoint written
-        before a bucket relayout loads after it).  Missing entries mean zero moments."""
+        before a bucket relayout loads after it).  Missing entries mean zero moments.  Returns
+        the stored hyperparameters {lr, betas, eps, weight_decay} (param_groups[0]); the
+        caller compares them with its own (TPGANTrainer.load_checkpoint)."""
         st = sd["state"]
         steps = {int(round(float(v["step"]))) for v in st.values()} or {0}
         if len(steps) != 1:
@@ -141,6 +143,9 @@ class FlatParams:
             self.adam_state.zero_()
             self.adam_state[0] = float(step)  # the next launch advances it and recomputes the corrections
         self.step = step
+        groups = sd.get("param_groups") or [{}]
+        g = groups[0]
+        return {k: (tuple(g[k]) if k == "betas" else g[k]) for k in ("lr", "betas", "eps", "weight_decay") if k in g}
 
     def weights_loaded(self):
         """After parameter values were overwritten in place (load_state_dict): rebuild the packed images."""
@@ -302,6 +307,12 @@ class OverlappedGradSync(GradSync):
         return super(OverlappedGradSync, self).allreduce(flat)
 
 
+def _hp_equal(a, b):
+    if isinstance(a, (tuple, list)) or isinstance(b, (tuple, list)):
+        return len(a) == len(b) and all(_hp_equal(x, y) for x, y in zip(a, b))
+    return abs(float(a) - float(b)) <= 1e-12 * max(1.0, abs(float(b)))
+
+
 def total_variation(x):
     return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
 
@@ -422,27 +433,58 @@ class TPGANTrainer:
     def _nets(self):
         return (("G", self.G, self.fG), ("D", self.D, self.fD))
 
+    def _rank(self):
+        return dist.get_rank(self.sync.group) if self.world > 1 else 0
+
     def save_checkpoint(self, dir, epoch):
+        """Rank 0 writes (every rank holds the same replica); each file goes to a temporary
+        name first and is renamed into place (os.replace, atomic on POSIX), so a reader never
+        sees a partial file; all ranks leave only after the files exist (barrier)."""
         import os
         torch.cuda.synchronize() if self.fG.data.is_cuda else None
-        for tag, net, flat in self._nets():
-            d = os.path.join(dir, tag)
-            os.makedirs(d, exist_ok=True)
+        payload = []
+        for tag, net, flat in self._nets():  # collective-free, but every rank walks the same state
             sd = {k: v.detach().cpu().contiguous().clone() for k, v in net.state_dict().items()}
-            torch.save(sd, os.path.join(d, "model_epoch_%s.pth" % epoch))
-            torch.save({"optimizer": flat.optimizer_state_dict(self.lr, self.betas), "model": sd, "epoch": epoch},
-                       os.path.join(d, "optimizer_epoch_%s.pth" % epoch))
+            payload.append((tag, sd, flat.optimizer_state_dict(self.lr, self.betas)))
+        if self._rank() == 0:
+            for tag, sd, opt in payload:
+                d = os.path.join(dir, tag)
+                os.makedirs(d, exist_ok=True)
+                for name, obj in (("model_epoch_%s.pth" % epoch, sd),
+                                  ("optimizer_epoch_%s.pth" % epoch, {"optimizer": opt, "model": sd, "epoch": epoch})):
+                    final = os.path.join(d, name)
+                    tmp = final + ".tmp%d" % os.getpid()
+                    torch.save(obj, tmp)
+                    os.replace(tmp, final)
+        if self.world > 1:
+            dist.barrier(group=self.sync.group)
 
-    def load_checkpoint(self, dir, epoch):
+    def load_checkpoint(self, dir, epoch, adopt_hparams=False):
         """Restore both networks and their Adam states; returns the stored epoch.  Loaded with
-        weights_only=True (nothing in the file is executed)."""
+        weights_only=True (nothing in the file is executed).  The file's optimizer
+        hyperparameters (lr, betas, eps, weight_decay; e.g. the reference's getOptimizer Adam,
+        UtilityMethods.py:30-36, betas (0.9, 0.999)) must match this trainer's, since the
+        restored moments were built under them: a mismatch raises ValueError, or, with
+        adopt_hparams=True, the trainer takes the stored lr and betas (eps 1e-8 and
+        weight_decay 0 are fixed here, so those must match either way)."""
         import os
+        if self.world > 1:  # the writer's files are complete before anyone reads
+            dist.barrier(group=self.sync.group)
         out = None
         for tag, net, flat in self._nets():
             ck = torch.load(os.path.join(dir, tag, "optimizer_epoch_%s.pth" % epoch), map_location="cpu",
                             weights_only=True)
+            hp = flat.load_optimizer_state_dict(ck["optimizer"])
+            mine = {"lr": self.lr, "betas": tuple(self.betas), "eps": 1e-8, "weight_decay": 0.0}
+            bad = {k: (hp[k], mine[k]) for k in hp if k in mine and not _hp_equal(hp[k], mine[k])}
+            fixed = {k: v for k, v in bad.items() if k in ("eps", "weight_decay")}
+            if bad and (not adopt_hparams or fixed):
+                raise ValueError("checkpoint %s/%s optimizer hyperparameters differ from the trainer's "
+                                 "(stored, trainer): %s" % (tag, epoch, bad))
+            if bad:
+                self.lr = float(hp.get("lr", self.lr))
+                self.betas = tuple(hp.get("betas", self.betas))
             net.load_state_dict(ck["model"])  # copies into the flat-buffer views
-            flat.load_optimizer_state_dict(ck["optimizer"])
             flat.weights_loaded()
             out = ck["epoch"]
         return out  # every rank reads the same files: replicas stay identical without a broadcast
