@@ -91,6 +91,8 @@ def main():
     tpgan_ops.reset_flops()
     trainer.step(batch)
     flops_step = sum(tpgan_ops.FLOPS.values())
+    if os.environ.get("TPG_TUNE_DUMP") and rank == 0:  # the weight-gradient tiles the autotuner picked
+        tpgan_ops.save_tuning(os.environ["TPG_TUNE_DUMP"])
     torch.cuda.synchronize()
     graphed = args.graph
     if graphed:

@@ -128,6 +128,23 @@ int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, 
 int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw,
                               void* ws, size_t ws_bytes, tpg_stream_t stream);
 
+/* Fused per-layer backward of tpg_conv2d_fwd's op (replaces aten convolution_backward of the
+ * nn.Conv2d / nn.ConvTranspose2d built at ModificationLayer.py:101 / :186, plus the activation
+ * backward of the layer's LeakyReLU / ReLU):
+ *   g  = gy * act'(y)          (y = the forward's saved output; written to g — with
+ *                               TPG_ACT_NONE g is gy itself and g may be empty)
+ *   dx = input gradient of g   (dx.data NULL: skipped)
+ *   dw += weight gradient      (dw.data NULL: skipped; desc.algo / ksplit as tpg_conv2d_bwd_filter)
+ *   dbias += sum of g          (NULL: skipped)
+ * For a stride-1 "same" zero-padded Conv2d the activation' is applied while the input
+ * gradient's halo is staged (the input-gradient launch writes g as it goes) and the bias sum
+ * rides on the weight-gradient launch (one MFMA against ones per fragment); other layers run
+ * tpg_act_bwd first.  w may be a pre-packed image (desc.flags WPACKED, bwd_data layout).
+ * g must have y's strides for the fused form. */
+int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, tpg_tensor y, tpg_tensor gy,
+                       tpg_tensor g, tpg_tensor dx, tpg_tensor dw, float* dbias, void* ws, size_t ws_bytes,
+                       tpg_stream_t stream);
+
 /* g = gy * act'(y) over logical [n, c, h, w]; dbias[c] += sum g (dbias may be NULL). */
 int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
                     tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, tpg_stream_t stream);

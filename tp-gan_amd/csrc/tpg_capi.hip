@@ -265,7 +265,9 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
       if (best < 0 || pad < best) { best = pad; bn = c; }
     }
   }
-  const int hcap = (int)rup((int64_t)bimg * (bth + sy - 1) * (btw + sx - 1), 8);
+  // (whole 16-pixel rows: the masked-gradient mode DMAs y into the halo buffer 16 pixels per
+  // wave instruction)
+  const int hcap = (int)rup((int64_t)bimg * (bth + sy - 1) * (btw + sx - 1), 16);
   const int hl = std::max(3, cdiv(hcap * 4, 512));
   const int cfg = halo_cfg(hl, bn);
   if (cfg < 0) return;
@@ -452,12 +454,29 @@ extern "C" size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op) {
 }
 
 // run a list of problems: pack -> [zero split-K] -> igemm -> [finalize]
+// Masked input-gradient mode of the halo kernel (tpg_conv2d_bwd): A = gy, M = the saved
+// output y, G = where g = gy * act'(y) goes (M's strides).
+struct HaloMask {
+  tpg_tensor M, G;
+  int act;
+  float slope;
+};
+
 static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, const tpg_tensor& W, const float* bias,
                          int bias_mod, const tpg_tensor& R, float res_scale, const tpg_tensor& Y, int act, float slope,
-                         char* ws, size_t ws_bytes, hipStream_t s, const char* packed = nullptr) {
+                         char* ws, size_t ws_bytes, hipStream_t s, const char* packed = nullptr,
+                         const HaloMask* mk = nullptr) {
   size_t need = probs_ws(v);
   if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
   const bool vA = vec_ok(A, dtype);
+  if (mk) {  // the mask mode has no generic-kernel fallback: decide before launching anything
+    if (v.size() != 1 || !v[0].halo || v[0].h.ntaps < 2 || (v[0].h.var & 2) || !vA) return -31;
+    const int64_t ext = (int64_t)(v[0].h.N - 1) * std::abs(A.stride[0]) + (int64_t)(v[0].h.A_H - 1) * std::abs(A.stride[2]) +
+                        (int64_t)(v[0].h.A_W - 1) * std::abs(A.stride[3]) + v[0].h.C + 64;
+    const int64_t extm = (int64_t)(v[0].h.N - 1) * mk->M.stride[0] + (int64_t)(v[0].h.A_H - 1) * mk->M.stride[2] +
+                         (int64_t)(v[0].h.A_W - 1) * mk->M.stride[3] + v[0].h.C + 64;
+    if (ext >= (1ll << 31) || extm >= (1ll << 31)) return -31;
+  }
   for (Prob& P : v) {
     if (!P.halo) continue;
     // the halo kernel takes 16-byte aligned channels-last rows and keeps 32-bit element
@@ -502,7 +521,11 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
       h.yvec = vec_ok(Y, dtype);
       h.rvec = R.data ? vec_ok(R, dtype) : 0;
       h.wvec = a.Nout % 4 == 0;
-      int e = launch_halo(h, dtype, P.hcfg, s);
+      if (mk) {
+        h.M = mk->M.data; h.m_sn = mk->M.stride[0]; h.m_sh = mk->M.stride[2]; h.m_sw = mk->M.stride[3];
+        h.G = mk->G.data; h.mact = mk->act; h.mslope = mk->slope;
+      }
+      int e = launch_halo(h, dtype, P.hcfg, s, mk != nullptr);
       if (e) return hip_check(e, "halo conv");
       if (h.ksplit > 1) {
         EpiArgs ep;
@@ -688,7 +711,7 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
 // Row-halo weight gradient (tpg_wgrad_rh.hip) for a stride-1 Conv2d: returns 1 when the
 // shape is not covered (caller falls back), else the launch status.
 static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_tensor& g, const tpg_tensor& dw,
-                        hipStream_t stream) {
+                        float* dbias, hipStream_t stream) {
   if (d->dtype != TPG_BF16 || d->stride_h != 1 || d->stride_w != 1) return 1;
   const int PH = d->out_h, PW = d->out_w, QH = d->in_h, QW = d->in_w;
   // row mode: one kernel row, 3/5/7 taps, 64-pixel row segments; image mode (algos 10, 11 and
@@ -764,12 +787,19 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   a.ksplit = cdiv(a.nkt, a.kt_per_split);
   a.dW = reinterpret_cast<float*>(dw.data);
   a.w_sa = dw.stride[0]; a.w_sb = dw.stride[1]; a.w_sr = dw.stride[2]; a.w_ss = dw.stride[3];
+  a.dbias = dbias;
+  // bias MFMAs spread over up to 16 / ksplit tiles: same-address atomics serialise (~50 ns
+  // each), so blocks x splits adding into one dbias row must stay few
+  a.bshare = deterministic() ? 1 : std::max(1, std::min(a.ntb * a.nrg * cdiv(a.kw, a.nt), 16 / a.ksplit));
   return hip_check(launch_wgrad_rh(a, stream), "wgrad_rh");
 }
 
-extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw, void* ws,
-                                         size_t ws_bytes, tpg_stream_t stream) {
-  (void)ws; (void)ws_bytes;
+// Weight gradient; with dbias (Conv2d only: the pixel-grid operand is g) the bias gradient is
+// summed by the same launch where the kernel supports it (*bias_done), else left to the caller.
+static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_tensor& g, const tpg_tensor& dw,
+                               float* dbias, bool* bias_done, tpg_stream_t stream) {
+  *bias_done = false;
+  if (d->transposed) dbias = nullptr;
   int32_t rc = check_desc(d);
   if (rc) return rc;
   if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(g, d->dtype, "g"))) return rc;
@@ -815,8 +845,11 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   static const bool rh_on = !getenv("TPG_WGRAD_RH") || atoi(getenv("TPG_WGRAD_RH")) != 0;  // A/B hook
   const bool rh_algo = d->algo >= 6 && d->algo <= 11;
   if (((d->algo == 0 && rh_on) || rh_algo) && !comp && !d->transposed) {
-    const int rc = wgrad_rh(d, x, g, dw, (hipStream_t)stream);
-    if (rc != 1) return rc;
+    const int rc = wgrad_rh(d, x, g, dw, dbias, (hipStream_t)stream);
+    if (rc != 1) {
+      *bias_done = rc == 0 && dbias != nullptr;
+      return rc;
+    }
   }
   if (rh_algo) return fail(-30, "wgrad: row-halo kernel does not apply to this shape");
   // pipelined DMA kernel when both operands are 16-byte aligned channels-last rows
@@ -876,7 +909,11 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
                 (int64_t)PH * PW > kp;
       a.dpy = kp / a.PW;
       a.dpx = kp % a.PW;
-      return hip_check(launch_wgrad2(a, d->dtype, wgrad2_cfg(bm, bn), bm, bn, (hipStream_t)stream), "wgrad2");
+      a.dbias = dbias;
+      a.bshare = deterministic() ? 1 : std::max(1, std::min((int)((ncols + bn - 1) / bn) * ngrid, 16 / a.ksplit));
+      const int32_t r2 = hip_check(launch_wgrad2(a, d->dtype, wgrad2_cfg(bm, bn), bm, bn, (hipStream_t)stream), "wgrad2");
+      *bias_done = r2 == 0 && dbias != nullptr;
+      return r2;
     }
   }
   const int cfg = (a.Ca >= 128 && a.Cb >= 128) ? 1 : 0;
@@ -888,6 +925,83 @@ extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, t
   a.pix_per_split = (int)rup(cdiv(a.npix, ks), 32);
   a.ksplit = cdiv(a.npix, a.pix_per_split);
   return hip_check(launch_wgrad(a, d->dtype, cfg, (hipStream_t)stream), "wgrad");
+}
+
+extern "C" int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g, tpg_tensor dw, void* ws,
+                                         size_t ws_bytes, tpg_stream_t stream) {
+  (void)ws; (void)ws_bytes;
+  bool bias_done;
+  return bwd_filter_impl(d, x, g, dw, nullptr, &bias_done, stream);
+}
+
+extern "C" int32_t tpg_colsum_impl(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor g, float* dbias,
+                                    hipStream_t s);
+
+// Fused per-layer backward (SURVEY.md §8b tpg_conv2d_bwd): g = gy * act'(y), dx, dw, dbias.
+extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, tpg_tensor y, tpg_tensor gy,
+                                  tpg_tensor g, tpg_tensor dx, tpg_tensor dw, float* dbias, void* ws, size_t ws_bytes,
+                                  tpg_stream_t stream) {
+  int32_t rc = check_desc(d);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (!gy.data) return fail(-10, "conv2d_bwd: gy is NULL");
+  const bool has_act = d->act != TPG_ACT_NONE;
+  if (has_act && !y.data) return fail(-10, "conv2d_bwd: y is NULL with an activation");
+  // without an activation g IS gy (when it already has the compute dtype)
+  // (16-byte aligned channels-last rows: the weight-gradient DMA kernels read g as it is)
+  const bool g_is_gy = !has_act && gy.dtype == d->dtype && vec_ok(gy, d->dtype);
+  if (!g_is_gy && (rc = check_tensor(g, d->dtype, "g"))) return rc;
+  const tpg_tensor& G = g_is_gy ? gy : g;
+  bool have_g = g_is_gy, bias_done = false, dx_done = false;
+  // pre-packed weights that the input-gradient plan of these tensors cannot use: report it
+  // (-21) before anything is launched, so the caller's retry with fp32 weights adds nothing twice
+  if ((d->flags & TPG_FLAG_WPACKED) && dx.data &&
+      (!vec_ok(G, d->dtype) || bwd_data_composite(d, &G, &dx) != bwd_data_composite(d, nullptr, nullptr)))
+    return fail(-21, "pre-packed weights assume the halo kernel / dense NHWC; these tensors need another plan");
+  // 1. the input gradient with the activation' applied while its halo is staged (writes g)
+  // (maps up to 64 x 64: there the separate activation-backward pass is latency-bound and the
+  // fusion wins; on the 128 x 128 layers it streams at ~5 TB/s and the masked staging costs as
+  // much as it saves (measured: 42.1 ms/step at 4096, 42.5 with every map, 43.0 with none))
+  static const int64_t mask_maxpix = getenv("TPG_MASK_MAXPIX") ? atoll(getenv("TPG_MASK_MAXPIX")) : 64 * 64;
+  if (!have_g && dx.data && !d->transposed && d->stride_h == 1 && d->stride_w == 1 && d->pad_mode == TPG_PAD_ZERO &&
+      (int64_t)d->out_h * d->out_w <= mask_maxpix &&
+      d->in_h == d->out_h && d->in_w == d->out_w && gy.dtype == d->dtype && y.dtype == d->dtype &&
+      dx.dtype == d->dtype && vec_ok(gy, d->dtype) && vec_ok(y, d->dtype) && vec_ok(g, d->dtype) &&
+      y.stride[0] == g.stride[0] && y.stride[2] == g.stride[2] && y.stride[3] == g.stride[3] &&
+      !getenv("TPG_NO_MASKED_DGRAD")) {
+    const bool packed = d->flags & TPG_FLAG_WPACKED;
+    if (w.data && (w.dtype == TPG_F32 || packed) && !bwd_data_composite(d, &gy, &dx)) {
+      std::vector<Prob> v = plan_bwd_data(d, false);
+      HaloMask mk;
+      mk.M = y; mk.G = g; mk.act = d->act; mk.slope = d->slope;
+      tpg_tensor none;
+      memset(&none, 0, sizeof(none));
+      rc = run_probs(v, d->dtype, gy, w, nullptr, 0, none, 0.f, dx, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws),
+                     ws_bytes, s, packed ? reinterpret_cast<const char*>(w.data) : nullptr, &mk);
+      if (rc == 0) have_g = dx_done = true;
+      else if (rc != -31) return rc;
+    }
+  }
+  // 2. otherwise the activation backward pass materialises g (and sums the bias)
+  if (!have_g) {
+    rc = hip_check(tpg_act_bwd_impl(d->n, d->out_c, d->out_h, d->out_w, d->act, d->slope, gy, y, g, dbias, s),
+                   "act_bwd");
+    if (rc) return rc;
+    have_g = true;
+    bias_done = dbias != nullptr;
+  }
+  if (dx.data && !dx_done) {
+    if ((rc = tpg_conv2d_bwd_data(d, G, w, dx, ws, ws_bytes, stream))) return rc;
+  }
+  // 3. the weight gradient, summing the bias gradient in the same launch where it can
+  if (dw.data) {
+    bool b = false;
+    if ((rc = bwd_filter_impl(d, x, G, dw, bias_done ? nullptr : dbias, &b, stream))) return rc;
+    bias_done = bias_done || b;
+  }
+  if (dbias && !bias_done)
+    return hip_check(tpg_colsum_impl(d->n, d->out_c, d->out_h, d->out_w, G, dbias, s), "colsum");
+  return 0;
 }
 
 extern "C" int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope, tpg_tensor gy,

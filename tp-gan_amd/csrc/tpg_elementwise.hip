@@ -224,6 +224,27 @@ __global__ __launch_bounds__(256) void act_bwd_vec_kernel(int64_t npix, int C, i
   }
 }
 
+// Column sums: dbias[c] += sum over pixels of g (the bias gradient where no other launch of
+// the fused backward summed it).  64 channels x 4 pixel lanes per block, any strides.
+__global__ __launch_bounds__(256) void colsum_kernel(int N, int C, int H, int W, tpg_tensor g, float* dbias) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int64_t npix = (int64_t)N * H * W;
+  float sum = 0.f;
+  if (c < C) {
+    for (int64_t pix = blockIdx.x * 4 + pl; pix < npix; pix += (int64_t)gridDim.x * 4) {
+      const int n = (int)(pix / ((int64_t)H * W));
+      const int rem = (int)(pix - (int64_t)n * H * W);
+      const int h = rem / W, w = rem - h * W;
+      sum += ld_any(g.data, g.dtype, n * g.stride[0] + c * g.stride[1] + h * g.stride[2] + w * g.stride[3]);
+    }
+  }
+  red[pl][cl] = sum;
+  __syncthreads();
+  if (pl == 0 && c < C) atomicAdd(dbias + c, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+}
+
 // ------------------------------------------------------------ strided 4-D copy --
 __global__ __launch_bounds__(256) void copy4d_kernel(int N, int C, int H, int W, tpg_tensor in, tpg_tensor out) {
   const int64_t total = (int64_t)N * C * H * W;
@@ -477,6 +498,15 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
   if (gx < 1 || (dbias && deterministic())) gx = 1;
   dim3 grid(gx, (c + 63) / 64);
   hipLaunchKernelGGL(act_bwd_kernel, grid, dim3(256), 0, s, n, c, h, w, act, slope, gy, y, g, dbias);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_colsum_impl(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor g, float* dbias,
+                                    hipStream_t s) {
+  const int64_t npix = (int64_t)n * h * w;
+  int gx = (int)std::min<int64_t>((npix + 63) / 64, 1024);
+  if (gx < 1 || deterministic()) gx = 1;
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, (c + 63) / 64), dim3(256), 0, s, n, c, h, w, g, dbias);
   return (int)hipGetLastError();
 }
 

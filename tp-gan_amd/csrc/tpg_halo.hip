@@ -61,7 +61,19 @@ __device__ __forceinline__ int h_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-template <bool BF, int HL, int BN, int WM, int WN>
+// g = gy * act'(y) on one 16-byte chunk of each (the masked input-gradient mode)
+template <typename E>
+__device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float slope) {
+  constexpr int N = 16 / sizeof(E);
+  union { u32x4 u; E e[N]; } a, b;
+  a.u = g;
+  b.u = y;
+#pragma unroll
+  for (int e = 0; e < N; ++e) a.e[e] = (E)tpg_act_grad((float)a.e[e], (float)b.e[e], act, slope);
+  return a.u;
+}
+
+template <bool BF, int HL, int BN, int WM, int WN, bool MASK>
 __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   using E = typename std::conditional<BF, __bf16, float>::type;
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
@@ -103,11 +115,16 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   // ---- per-thread halo slots (fixed across k-steps): element offset from A (absolute,
   // < 2^31 by the planner), negative = outside the image or a dead sub-tile -> zero
   int hoff[HL];
+  // mask mode: M / G pixel offset of each slot's pixel (-1 = none) and the slots whose pixel is
+  // one of this block's own output pixels (bit q; only the blockIdx.y == 0 blocks store g)
+  int mpix[MASK ? HL : 1];
+  uint32_t core = 0;
 #pragma unroll
   for (int q = 0; q < HL; ++q) {
     const int idx = tid + 512 * q;
     const int hp = idx >> 2, ch = idx & 3;
     hoff[q] = -1;
+    if constexpr (MASK) mpix[q] = -1;
     if (hp < IMG * HP) {
       const int sub = hp / HP, hl = hp - sub * HP;
       const int st = st0 + sub;
@@ -117,8 +134,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
         const int hy = hl / HW, hx = hl - hy * HW;
         int gy = ty * TH * SH + p.dymin + hy, gx = tx * TW * SW + p.dxmin + hx;
         if (p.pad_mode) { gy = h_refl(gy, p.A_H); gx = h_refl(gx, p.A_W); }
-        if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W)
+        if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W) {
           hoff[q] = (int)((int64_t)nimg * p.a_sn + gy * p.a_sh + gx * p.a_sw) + ch * EPC;
+          if constexpr (MASK) {
+            mpix[q] = (int)((int64_t)nimg * p.m_sn + gy * p.m_sh + gx * p.m_sw);
+            const int cy = gy - ty * TH, cx = gx - tx * TW;  // (SH = SW = 1 in this mode)
+            if (blockIdx.y == 0 && (unsigned)cy < (unsigned)TH && (unsigned)cx < (unsigned)TW) core |= 1u << q;
+          }
+        }
       }
     }
   }
@@ -138,15 +161,57 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
       hreg[q] = *reinterpret_cast<const u32x4*>(Ag + (ok ? hoff[q] + cbase : 0));
     }
   };
+  int gch = 0;  // mask mode: channel of this thread's chunks in the last stored halo
   auto store_halo = [&](int buf) {
     u32x4* H = halo + buf * hcap * 4;
 #pragma unroll
     for (int q = 0; q < HL; ++q) {
       const int idx = tid + 512 * q;
       const int hp = idx >> 2;
-      u32x4 v = mask_chunk4<EPC>(hreg[q], hc, p.C);
+      const int pos = hp * 4 + ((idx & 3) ^ hswz(hp));
+      u32x4 v = hreg[q];
+      if constexpr (MASK) {
+        if (hp < HPT) v = act_mask_chunk<E>(v, H[pos], p.mact, p.mslope);  // y chunk, DMA'd in place
+      }
+      v = mask_chunk4<EPC>(v, hc, p.C);
       if (hoff[q] < 0) v = u32x4{0u, 0u, 0u, 0u};
-      if (hp < HPT) H[hp * 4 + ((idx & 3) ^ hswz(hp))] = v;
+      if (hp < HPT) H[pos] = v;
+      if constexpr (MASK) hreg[q] = v;
+    }
+    if constexpr (MASK) gch = hc;
+  };
+  // mask mode: LDS-DMA of y's chunks of k-step ks into halo buffer buf, at the positions the
+  // halo chunks will take (lane-linear DMA: the lane landing at position idx fetches pixel
+  // idx >> 2, logical chunk (idx & 3) ^ hswz(pixel)); store_halo reads them back, masks and
+  // overwrites them.  Invalid pixels fetch element 0 (their g is zeroed anyway).
+  const E* Mg = reinterpret_cast<const E*>(p.M);
+  auto issue_m = [&](int ks, int buf) {
+    if constexpr (MASK) {
+      const int cbase = (ks0 + ks) * KS;
+      char* dst = reinterpret_cast<char*>(halo + buf * hcap * 4);
+#pragma unroll
+      for (int q = 0; q < HL; ++q) {
+        const int idx = tid + 512 * q;
+        const int hp = idx >> 2;
+        const int c = cbase + (((idx & 3) ^ hswz(hp)) * EPC);
+        const E* src = Mg + ((mpix[q] >= 0 && c < p.C) ? mpix[q] + c : 0);
+        if ((512 * q + 64 * wave) / 4 < hcap)  // wave-uniform; hcap % 16 == 0: the instruction stays inside the buffer
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)(dst + (512 * q + 64 * wave) * 16),
+                                           16, 0, 0);
+      }
+    }
+  };
+  // mask mode: the masked chunks of the block's own pixels go to G (issued at the start of the
+  // next pipeline step, so the stores are the oldest vector-memory operations of that step)
+  E* Gg = reinterpret_cast<E*>(p.G);
+  auto store_g = [&]() {
+    if constexpr (MASK) {
+      if (gch < p.C) {
+#pragma unroll
+        for (int q = 0; q < HL; ++q)
+          if ((core >> q) & 1u) *reinterpret_cast<u32x4*>(Gg + mpix[q] + gch) = hreg[q];
+      }
     }
   };
   // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
@@ -262,7 +327,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   const int total = nks * ntaps;
   __syncthreads();  // tap table
   if ((p.var & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  if (total > 0 && RS == 4) {
+  if (total > 0 && RS == 4 && !MASK) {
     // 4-slot ring: step s+3's weights are issued at the start of step s
     load_halo(0);
     issue_w(0, 0);
@@ -288,15 +353,23 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (total > 0) {
     load_halo(0);
+    issue_m(0, 0);
     issue_w(0, 0);
     issue_w(min(1, total - 1), 1);
+    if constexpr (MASK) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // y chunks landed
     store_halo(0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     int ks = 0, t = 0, slot = 0;
     int toff = s_toff[0];
     for (int s = 0; s < total; ++s) {
       const bool more_ks = ks + 1 < nks;
-      if (t == 0 && more_ks) load_halo(ks + 1);
+      if (t == 0) {
+        store_g();  // g of k-step ks (staged at the end of the previous one)
+        if (more_ks) {
+          load_halo(ks + 1);
+          issue_m(ks + 1, (ks + 1) & 1);  // that buffer was last read in k-step ks - 1
+        }
+      }
       const int slot2 = slot == 0 ? 2 : slot - 1;  // (s + 2) % 3
       issue_w(min(s + 2, total - 1), slot2);
       const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];  // read ahead of its use
@@ -487,9 +560,9 @@ size_t halo_lds_bytes(int hcap, int bn, int rs) {
   return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn));
 }
 
-template <bool BF, int HL, int BN, int WM, int WN>
+template <bool BF, int HL, int BN, int WM, int WN, bool MASK>
 static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
-  auto k = halo_kernel<BF, HL, BN, WM, WN>;
+  auto k = halo_kernel<BF, HL, BN, WM, WN, MASK>;
   const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3);
   const int maxl = (int)halo_lds_bytes(HL * 128, BN, 4);
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
@@ -499,13 +572,18 @@ static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s) {
+int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask) {
   dim3 grid((a.N * a.tiles_h * a.tiles_w + a.IMG - 1) / a.IMG, a.ntiles, a.ksplit);
-#define X(id, HL_, BN_, WM_, WN_)                                         \
-  if (cfg == (id)) {                                                      \
-    if (a.hcap > HL_ * 128) return -1;                                    \
-    return dtype == 1 ? launch_halo_t<true, HL_, BN_, WM_, WN_>(a, grid, s) \
-                      : launch_halo_t<false, HL_, BN_, WM_, WN_>(a, grid, s); \
+  // mask mode: one k-step's y chunks must land (LDS-DMA issued at tap 0) before its halo is
+  // staged (last tap): at least two taps, the 3-slot ring, whole 16-pixel DMA rows
+  if (mask && (a.ntaps < 2 || (a.var & 2) || a.hcap % 16 || a.SH != 1 || a.SW != 1)) return -1;
+#define X(id, HL_, BN_, WM_, WN_)                                                       \
+  if (cfg == (id)) {                                                                    \
+    if (a.hcap > HL_ * 128) return -1;                                                  \
+    if (mask) return dtype == 1 ? launch_halo_t<true, HL_, BN_, WM_, WN_, true>(a, grid, s)  \
+                                : launch_halo_t<false, HL_, BN_, WM_, WN_, true>(a, grid, s); \
+    return dtype == 1 ? launch_halo_t<true, HL_, BN_, WM_, WN_, false>(a, grid, s)      \
+                      : launch_halo_t<false, HL_, BN_, WM_, WN_, false>(a, grid, s);    \
   }
   TPG_HALO_CFGS(X)
 #undef X

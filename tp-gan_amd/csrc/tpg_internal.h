@@ -117,6 +117,8 @@ struct WgradArgs {
   FastDiv div_pw, div_phpw;
   int8_t dy[TPG_MAX_TAPS], dx[TPG_MAX_TAPS], tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
   int p_bytes, q_bytes;       // buffer extents for the DMA kernel (out-of-range reads -> 0)
+  float* dbias;               // wgrad2 only, P = dY (Conv2d): dbias[a] += sum_p P[p][a] (may be null)
+  int bshare;                 // k-tiles' bias sums spread over this many column tiles (1 = tile 0 only)
   int bflat, cbp;             // wgrad2 tap-flattened columns: b' = tap * cbp + b, cbp = rup(Cb, 8)
   int fastp;                  // P dense NHWC: DMA offset = pixel * p_sw + c, no division
   int fastq;                  // Q dense, same grid as P, unit stride, zero pad, image > one k-tile:
@@ -141,6 +143,10 @@ struct WgradRHArgs {
   int nkt, kt_per_split, ksplit;
   float* dW;
   int64_t w_sa, w_sb, w_sr, w_ss;
+  float* dbias;               // dbias[a] += sum_p dY[p][a] (may be null): one MFMA against ones per
+                              // A fragment; k-tile kt is summed by tile (kt % bshare) of the a-tile's
+                              // (b, row, tap) tiles (bshare = 1: the first one, deterministic)
+  int bshare;
 };
 
 // ---------------------------------------------------------------- weight packing ----
@@ -294,6 +300,16 @@ struct HaloArgs {
   int var;                    // pipeline variant bits (TPG_HALO_VAR, tuning): 1 = waves 4-7 at
                               // priority 1, 2 = 4-slot weight ring (DMA three steps ahead),
                               // 8 = no wave stagger (bf16 BN >= 128 tiles stagger waves 4-7)
+  // Masked input-gradient mode (launch_halo(..., mask = true); stride-1 "same" Conv2d dgrad):
+  // A holds the incoming gradient gy, M the conv's saved output y (same grid); the halo is
+  // staged as g = gy * act'(y) (mact / mslope), and every g chunk of the block's own output
+  // pixels (blockIdx.y == 0) is also stored to G (G has M's strides), so the weight gradient
+  // can read g without a separate activation-backward pass.
+  const void* M;
+  int64_t m_sn, m_sh, m_sw;
+  void* G;
+  int mact;
+  float mslope;
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 
@@ -319,7 +335,7 @@ int launch_wgrad_rh(const WgradRHArgs& a, hipStream_t s);
 int wgrad_rh_tile(int cfg, int* bm, int* bc);
 int halo_cfg(int hl, int bn);
 size_t halo_lds_bytes(int hcap, int bn, int rs = 3);
-int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s);
+int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask = false);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
 

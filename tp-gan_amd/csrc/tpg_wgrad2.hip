@@ -22,6 +22,7 @@ namespace tpg {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4r;
 
 __device__ __forceinline__ int w2_refl(int i, int n) {
   i = i < 0 ? -i : i;
@@ -214,13 +215,21 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, l16 = lane & 15;
-  f32x4 acc[MREP][NREP];
+  // bias gradient (P = dY): the first column tile (and tap) sees every pixel of the split once
+  // (k-tile kt goes to the column tile with share index kt % bshare; bshare = 1: tile 0 only)
+  const int sid = tb + ntb * (FLAT ? 0 : tap);
+  const bool bias_wave = p.dbias != nullptr && sid < p.bshare && wn == 0;
+  const int kt_base = pbeg / KP;
+  f32x4 acc[MREP][NREP], accb[MREP];
 #pragma unroll
-  for (int m = 0; m < MREP; ++m)
+  for (int m = 0; m < MREP; ++m) {
+    accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
 
-  auto compute = [&](int slot) {
+  auto compute = [&](int slot, bool bias_now) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     if constexpr (BF) {
@@ -266,6 +275,15 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        if (bias_now) {
+#pragma unroll
+          for (int m = 0; m < MREP; ++m) {
+            const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
+                                                                                 0, 1, 2, 3, 4, 5, 6, 7));
+            accb[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, ones, accb[m], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
         if (ks + 1 < NS) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
@@ -291,6 +309,10 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 #pragma unroll
           for (int n = 0; n < NREP; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+        if (bias_now) {
+#pragma unroll
+          for (int m = 0; m < MREP; ++m) accb[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], 1.0f, accb[m], 0, 0, 0);
+        }
       }
     }
   };
@@ -312,7 +334,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
     for (int kt = 0; kt < nkt; ++kt) {
       const int slot2 = slot == 0 ? 2 : slot - 1;
       issue(min(kt + 2, nkt - 1), slot2);  // unconditional (clamped): static vmcnt
-      compute(slot);
+      compute(slot, bias_wave && (kt_base + kt) % p.bshare == sid);
       W2_WAIT_BARRIER();                   // retires k-tile kt+1, kt+2 stays in flight
       slot = slot == 2 ? 0 : slot + 1;
     }
@@ -351,6 +373,17 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
         else atomicAdd(dst, acc[m][n][reg]);
       }
     }
+  if (bias_wave && l16 == 0) {  // every column of accb holds the row sum
+#pragma unroll
+    for (int m = 0; m < MREP; ++m)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int a = a0 + wm * WTM + m * 16 + 4 * g + reg;
+        if (a >= p.Ca) continue;
+        if (p.ksplit == 1 && p.bshare == 1) p.dbias[a] += accb[m][reg];
+        else atomicAdd(p.dbias + a, accb[m][reg]);
+      }
+  }
 }
 
 // {id, BM, BN, WM, WN}

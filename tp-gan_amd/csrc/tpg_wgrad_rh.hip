@@ -22,6 +22,7 @@ namespace tpg {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4r;
 
 __device__ __forceinline__ s16x4 rh_tr_read(const char* p) {
   s16x4 v;
@@ -84,6 +85,12 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   const int kt0 = split * p.kt_per_split;
   const int nkt = min(p.nkt, kt0 + p.kt_per_split) - kt0;
   if (nkt <= 0) return;
+  // bias gradient: the blocks of the first b tile, kernel row group and tap group see every
+  // dY pixel of their split exactly once; one wave column of them sums the A fragments
+  // (k-tile kt of the split is summed by the tile with share index kt % bshare, so the extra
+  // MFMAs spread evenly over the a-tile's blocks; bshare = 1 keeps one owner: deterministic)
+  const int sid = tb + p.ntb * (t % p.nrg + p.nrg * (t / p.nrg));
+  const bool has_bias = p.dbias != nullptr && sid < p.bshare;
 
   // position of k-tile kt0: (n, py, px0), advanced incrementally (all scalar)
   // TH = floor(64 / TW): pixels TH*TW..63 of a k-tile are dead (zero dY rows), and a last
@@ -149,11 +156,15 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, l16 = lane & 15;
   const int q = l16 >> 2, p4 = l16 & 3;
-  f32x4 acc[MREP][NREP];
+  const bool bias_wave = has_bias && wn == 0;
+  f32x4 acc[MREP][NREP], accb[MREP];
 #pragma unroll
-  for (int m = 0; m < MREP; ++m)
+  for (int m = 0; m < MREP; ++m) {
+    accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < NREP; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});  // 1.0 bf16
 
   // Fragment reads (transposed, 4 channels x 4 pixels per lane and read): fragment r < 2*MREP
   // is dY (A), the rest X halo rows shifted by the column's tap.  Next substep's reads are
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       const int k = ks * 32 + 8 * g + 4 * h + q;
       kbase[ks][h] = (k / TW) * HW + k % TW;
     }
-  auto compute = [&](int slot) {
+  auto compute = [&](int slot, bool bias_now) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     constexpr int NS = KP / 32;
@@ -207,6 +218,15 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (bias_now) {  // dbias: the substep's A fragments against ones (h[cur] is not overwritten yet)
+#pragma unroll
+        for (int m = 0; m < MREP; ++m) {
+          const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
+                                                                               0, 1, 2, 3, 4, 5, 6, 7));
+          accb[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, ones, accb[m], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (ks + 1 < NS) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -236,7 +256,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   int slot = 0;
   for (int kt = 0; kt < nkt; ++kt) {
     issue_next(slot == 0 ? 2 : slot - 1);
-    compute(slot);
+    compute(slot, bias_wave && (kt0 + kt) % p.bshare == sid);
     RH_WAIT_BARRIER();  // retires k-tile kt+1, kt+2 stays in flight
     slot = slot == 2 ? 0 : slot + 1;
   }
@@ -261,6 +281,17 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         else atomicAdd(dst, acc[m][j][reg]);
       }
     }
+  if (bias_wave && l16 == 0) {  // every column of accb holds the row sum
+#pragma unroll
+    for (int m = 0; m < MREP; ++m)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int a = a0 + wm * WTM + m * 16 + 4 * g + reg;
+        if (a >= p.Ca) continue;
+        if (p.ksplit == 1 && p.bshare == 1) p.dbias[a] += accb[m][reg];
+        else atomicAdd(p.dbias + a, accb[m][reg]);
+      }
+  }
 }
 
 // tile configs {id, BM, BC}; id = desc.algo - 6 (ids 4, 5: image mode, 32-channel b tiles)

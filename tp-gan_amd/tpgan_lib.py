@@ -45,6 +45,9 @@ EXPORTS = {
                                              ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "tpg_conv2d_bwd_filter": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor,
                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "tpg_conv2d_bwd": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor, TpgTensor,
+                                        TpgTensor, TpgTensor, TpgTensor, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_size_t, ctypes.c_void_p]),
     "tpg_act_bwd": (ctypes.c_int32, [ctypes.c_int32] * 5 + [ctypes.c_float, TpgTensor, TpgTensor, TpgTensor,
                                                              ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_copy4d": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor, ctypes.c_void_p]),

@@ -46,11 +46,12 @@ def _probe_begin(d, which):
     return e0
 
 
-def _probe_end(e0, d, which=""):
+def _probe_end(e0, d, which="", work=None):
     if e0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        work = _conv_flops(d) if which != "actb" else 6 * d.n * d.out_h * d.out_w * d.out_c  # bytes for act'
+        if work is None:
+            work = _conv_flops(d) if which != "actb" else 6 * d.n * d.out_h * d.out_w * d.out_c  # bytes for act'
         PROBE["events"].append((e0, e1, work, which, desc_key(d)))
 
 
@@ -410,6 +411,8 @@ class _ConvAct(torch.autograd.Function):
     def backward(ctx, gy):
         if torch.is_grad_enabled():  # create_graph=True (WGAN-GP): differentiable backward
             return _conv_act_backward_graph(ctx, gy)
+        if FUSED_BWD["enabled"]:
+            return _conv_act_backward_fused(ctx, gy)
         lib = load()
         x, weight, y = ctx.saved_tensors
         d = ctx.d
@@ -471,6 +474,89 @@ class _ConvAct(torch.autograd.Function):
             if dres.dtype != ctx.res_dtype:
                 dres = dres.to(ctx.res_dtype)
         return dx, dw, dbias, dres, None, None, None, None, None
+
+
+# Fused per-layer backward (tpg_conv2d_bwd): one C-ABI call per layer instead of
+# act_bwd + bwd_data + bwd_filter; for stride-1 "same" convs the activation' is applied in
+# the input-gradient kernel's halo staging and the bias gradient rides on the weight-gradient
+# kernel.  FUSED_BWD["enabled"] = False restores the three-call path (A/B, tests).
+FUSED_BWD = {"enabled": True}
+
+
+def _conv_act_backward_fused(ctx, gy):
+    lib = load()
+    x, weight, y = ctx.saved_tensors
+    d = ctx.d
+    dtype = y.dtype
+    n, cout, oh, ow = y.shape
+    need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+    need_db = ctx.has_bias and ctx.needs_input_grad[2]
+    gy = _fix_c1(gy)
+    es = 2 if dtype == torch.bfloat16 else 4
+    g_is_gy = (ctx.act == ACT_NONE and gy.dtype == dtype and gy.dim() == 4 and gy.stride(1) == 1 and
+               gy.data_ptr() % 16 == 0 and all((gy.stride(i) * es) % 16 == 0 for i in (0, 2, 3)))
+    g = gy if g_is_gy else _fix_c1(new_act(n, cout, oh, ow, dtype, y.device))
+    dbias = None
+    fused_b = False
+    if need_db:
+        fused_b = _fused_target(ctx.bparam) is not None
+        dbias = ctx.bparam.grad if fused_b else torch.zeros(cout, dtype=torch.float32, device=y.device)
+    dx = new_act(*x.shape, dtype=dtype, device=x.device) if need_dx else None
+    dw = dwv = None
+    if need_dw:
+        tgt = _fused_target(ctx.wparam)
+        if tgt is not None:  # dW accumulates straight into the flat gradient buffer
+            dwv = tgt if tgt.shape == weight.shape else tgt.view(weight.shape)
+        else:
+            dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
+            if weight.dim() == 4 and weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous(memory_format=torch.channels_last)
+            dwv = dw
+    wv = weight if weight.dtype == torch.float32 else weight.float()
+    ws = _ws(lib, d, OP_BWD_DATA, x.device) if need_dx else None
+    wsp, wsn = (ws.data_ptr(), ws.numel()) if ws is not None else (None, 0)
+    # the weight-gradient tile / split is autotuned on a shape's first call, which needs g:
+    # that call runs the fused op without dW, tunes on its g, then runs the weight gradient
+    key = ("wgrad", _desc_tuple(d))
+    tune_first = (need_dw and AUTOTUNE["enabled"] and d.dtype == TPG_BF16 and key not in AUTOTUNE["cache"])
+    if need_dw and not tune_first:
+        d.algo, d.ksplit = AUTOTUNE["cache"].get(key, (0, 0))
+    if need_dx:
+        FLOPS["dgrad"] += _conv_flops(d)
+    if need_dw:
+        FLOPS["wgrad"] += _conv_flops(d)
+    pk = _packed_weight(ctx.wparam, d, OP_BWD_DATA, wv) if need_dx else None
+    fx = _fix_c1(dx) if dx is not None else None
+    dwt = dwv if (need_dw and not tune_first) else None
+    bptr = dbias.data_ptr() if dbias is not None else None
+    e0 = _probe_begin(d, "bwd")
+    _run_maybe_packed(
+        lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk), tt(y), tt(gy), tt(g), tt(fx), tt(dwt), bptr,
+                                   wsp, wsn, stream_ptr()),
+        lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), tt(wv), tt(y), tt(gy), tt(g), tt(fx), tt(dwt), bptr,
+                                   wsp, wsn, stream_ptr()), d, pk)
+    _probe_end(e0, d, "bwd", _conv_flops(d) * (int(bool(need_dx)) + int(bool(need_dw and not tune_first))))
+    if tune_first:
+        algo, ks = _tuned_wgrad(lib, d, x, g, dwv)
+        d.algo, d.ksplit = algo, ks
+        check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dwv), None, 0, stream_ptr()))
+    d.algo, d.ksplit = 0, 0
+    if fused_b:
+        dbias = None  # accumulated straight into bias.grad
+        _grad_ready(ctx.bparam)
+    if need_dw:
+        if dw is None:
+            _grad_ready(ctx.wparam)
+        elif dw.dtype != weight.dtype:
+            dw = dw.to(weight.dtype)
+    if dx is not None and dx.dtype != ctx.in_dtype:
+        dx = dx.to(ctx.in_dtype)
+    dres = None
+    if ctx.has_res and ctx.needs_input_grad[3]:
+        dres = g if ctx.res_scale == 1.0 else g * ctx.res_scale
+        if dres.dtype != ctx.res_dtype:
+            dres = dres.to(ctx.res_dtype)
+    return dx, dw, dbias, dres, None, None, None, None, None
 
 
 # ---- double backward (WGAN-GP): the backward of _ConvAct written as
