@@ -94,7 +94,8 @@ typedef struct tpg_conv_desc {
                                      tpg_pack_run produced for this descriptor and op */
 } tpg_conv_desc;
 
-enum { TPG_FLAG_WPACKED = 1 };
+enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2 };  /* CONCURRENT: the op runs beside other
+                                  streams' work (plan grids for a quarter of the chip: fewer splits) */
 
 /* Workspace bytes needed by op (TPG_OP_*) for this descriptor. */
 size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op);

@@ -256,7 +256,7 @@ class Generator(nn.Module):
             outs = []
             for st, path, x in zip(side, paths, patches):
                 st.wait_stream(main)
-                with torch.cuda.stream(st):
+                with torch.cuda.stream(st), tpgan_ops.concurrent():
                     outs.append(path(x))
             enc = self.global_pathway.encode(I128, z)
             for st, (img, feat) in zip(side, outs):

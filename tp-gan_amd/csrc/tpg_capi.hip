@@ -43,6 +43,16 @@ using namespace tpg;
 static thread_local std::string g_err;
 static int g_det = 0;  // tpg_set_deterministic
 
+// Share of the chip an op plans its grid for: 1, or 4 when desc.flags has TPG_FLAG_CONCURRENT
+// (the op runs beside other streams' work, e.g. the four local pathways: fewer K / pixel
+// splits, since the other streams fill the CUs a split would).  Set per entry point.
+static thread_local int g_share = 1;
+struct ShareScope {
+  int prev;
+  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share) { g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? 4 : 1; }
+  ~ShareScope() { g_share = prev; }
+};
+
 int tpg::deterministic() { return __atomic_load_n(&g_det, __ATOMIC_RELAXED); }
 
 static int32_t fail(int32_t code, const char* fmt, ...) {
@@ -107,8 +117,8 @@ static void finish(Prob& P, int dtype, int M) {
   const int blocks = cdiv(M, bm) * (npad / bn);
   a.ksplit = 1;
   a.kt_per_split = std::max(nkt, 1);
-  if (blocks < 480 && nkt >= 8 && !deterministic()) {
-    int ks = std::min(cdiv(960, blocks), nkt / 4);
+  if (blocks < 480 / g_share && nkt >= 8 && !deterministic()) {
+    int ks = std::min(cdiv(960 / g_share, blocks), nkt / 4);
     if (ks > 1) {
       a.kt_per_split = cdiv(nkt, ks);
       a.ksplit = cdiv(nkt, a.kt_per_split);
@@ -297,9 +307,9 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   static const int split_steps = getenv("TPG_SPLIT_STEPS") ? atoi(getenv("TPG_SPLIT_STEPS")) : 4;
   // (deterministic mode: no k-split at all, so a sample's outputs are summed in the same
   // order whatever the batch size — the DP run then matches the 1-GPU run at its global batch)
-  if (base < split_below && !deterministic()) {
+  if (base < split_below / g_share && !deterministic()) {
     const int kps_min = cdiv(split_steps, a.ntaps);
-    ks = (int)std::min<int64_t>(cdiv(split_to, (int)base), std::max(1, h.nks / kps_min));
+    ks = (int)std::min<int64_t>(cdiv(split_to / g_share, (int)base), std::max(1, h.nks / kps_min));
   }
   h.kps = cdiv(h.nks, std::max(ks, 1));
   h.ksplit = cdiv(h.nks, h.kps);
@@ -439,6 +449,7 @@ static size_t reflect_tmp_bytes(const tpg_conv_desc* d) {
 }
 
 extern "C" size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op) {
+  ShareScope share_scope(d);
   if (check_desc(d)) return 0;
   if (op == TPG_OP_FWD) {
     size_t a = probs_ws(plan_fwd(d, false));
@@ -594,6 +605,7 @@ static std::vector<Prob> pack_plan(const tpg_conv_desc* d, int32_t op) {
 }
 
 extern "C" size_t tpg_conv2d_packed_bytes(const tpg_conv_desc* d, int32_t op) {
+  ShareScope share_scope(d);
   if (check_desc(d) || (op != TPG_OP_FWD && op != TPG_OP_BWD_DATA)) return 0;
   size_t b = 0;
   for (const Prob& P : pack_plan(d, op)) b += std::max(P.wp_bytes, P.g_wp);
@@ -604,6 +616,7 @@ extern "C" size_t tpg_pack_job_bytes(void) { return sizeof(PackJob); }
 
 extern "C" int32_t tpg_conv2d_pack_jobs(const tpg_conv_desc* d, int32_t op, tpg_tensor w, void* wp, void* jobs,
                                         int32_t max_jobs) {
+  ShareScope share_scope(d);
   int32_t rc = check_desc(d);
   if (rc) return rc;
   if (op != TPG_OP_FWD && op != TPG_OP_BWD_DATA) return fail(-2, "pack: op must be fwd or bwd_data");
@@ -657,6 +670,7 @@ extern "C" int32_t tpg_pack_run(const void* jobs_dev, int32_t n, int64_t nblocks
 
 extern "C" int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, const float* bias,
                                   tpg_tensor residual, tpg_tensor y, void* ws, size_t ws_bytes, tpg_stream_t stream) {
+  ShareScope share_scope(d);
   int32_t rc = check_desc(d);
   if (rc) return rc;
   if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(y, d->dtype, "y"))) return rc;
@@ -676,6 +690,7 @@ extern "C" int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
 
 extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx, void* ws,
                                        size_t ws_bytes, tpg_stream_t stream) {
+  ShareScope share_scope(d);
   int32_t rc = check_desc(d);
   if (rc) return rc;
   if ((rc = check_tensor(g, d->dtype, "g")) || (rc = check_tensor(dx, d->dtype, "dx"))) return rc;
@@ -769,7 +784,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   } else {
     // pixel splits: whole rounds of resident blocks (one per CU, two for the <= 128-VGPR
     // tiles) against the fp32 atomics every extra split adds (~1.3 TB/s of added bytes)
-    const int resident = img ? 256 : (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256;
+    const int resident = (img ? 256 : (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256) / g_share;
     const int taps = a.nr * a.nt;
     const double flops = 2.0 * a.tiles * bm * taps * bc * 64.0 * a.nkt;
     double best = -1;
@@ -798,6 +813,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
 // summed by the same launch where the kernel supports it (*bias_done), else left to the caller.
 static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_tensor& g, const tpg_tensor& dw,
                                float* dbias, bool* bias_done, tpg_stream_t stream) {
+  ShareScope share_scope(d);
   *bias_done = false;
   if (d->transposed) dbias = nullptr;
   int32_t rc = check_desc(d);
@@ -874,7 +890,7 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
         if (best < 0 || cost < best) { best = cost; bm = c[0]; bn = c[1]; }
       }
       const int tiles = cdiv(a.Ca, bm) * (int)((ncols + bn - 1) / bn) * ngrid;
-      bks = std::max(1, cdiv(2048, tiles));
+      bks = std::max(1, cdiv(2048 / g_share, tiles));
       bks = std::min(bks, std::max(1, a.npix / (kp * 8)));
     }
     if (d->algo >= 1 && d->algo <= 5 && d->ksplit >= 1) {
@@ -941,6 +957,7 @@ extern "C" int32_t tpg_colsum_impl(int32_t n, int32_t c, int32_t h, int32_t w, t
 extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, tpg_tensor y, tpg_tensor gy,
                                   tpg_tensor g, tpg_tensor dx, tpg_tensor dw, float* dbias, void* ws, size_t ws_bytes,
                                   tpg_stream_t stream) {
+  ShareScope share_scope(d);
   int32_t rc = check_desc(d);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;

@@ -35,6 +35,7 @@ class ConvDesc(ctypes.Structure):
 
 
 FLAG_WPACKED = 1
+FLAG_CONCURRENT = 2
 
 
 EXPORTS = {

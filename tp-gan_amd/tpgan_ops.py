@@ -16,7 +16,8 @@ import os
 
 import torch
 
-from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_WPACKED, OP_BWD_DATA, OP_FWD, PAD_REFLECT,
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
+                       PAD_REFLECT,
                        PAD_ZERO, TPG_BF16, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load, stream_ptr, tt)
 
 _DTYPE = [torch.float32]
@@ -95,6 +96,19 @@ def deterministic(on=True):
 
 # Run the Generator's four local pathways on side streams (D_and_G_model.Generator).
 MULTISTREAM = os.environ.get("TPG_MULTISTREAM", "1") != "0"
+# Ops created inside `concurrent()` carry TPG_FLAG_CONCURRENT: their grids are planned for a
+# share of the chip (the side-stream local pathways), forward and backward.
+_CONCURRENT = [False]
+CONCURRENT_HINT = {"enabled": os.environ.get("TPG_CONCURRENT_HINT", "1") != "0"}
+
+
+@contextlib.contextmanager
+def concurrent(on=True):
+    _CONCURRENT.append(bool(on) and CONCURRENT_HINT["enabled"])
+    try:
+        yield
+    finally:
+        _CONCURRENT.pop()
 _SIDE = {}
 
 
@@ -186,6 +200,7 @@ class ConvGeom:
         d.slope = slope
         d.res_scale = res_scale
         d.ksplit = 0
+        d.flags = FLAG_CONCURRENT if _CONCURRENT[-1] else 0
         return d
 
 
@@ -212,12 +227,17 @@ def load_tuning(path):
     import json
     with open(path) as f:
         for key, op, v in json.load(f):
-            AUTOTUNE["cache"][(op, tuple(key))] = tuple(v)
+            AUTOTUNE["cache"][(op, tuple(key))] = tuple(v)  # (tuples of _wgrad_key: shape + concurrency flag)
+
+
+def _wgrad_key(d):
+    return ("wgrad", _desc_tuple(d) + (int(d.flags & FLAG_CONCURRENT),))
 
 
 def _tuned_wgrad(lib, d, x, g, dwv):
-    """(algo, ksplit) for this weight-gradient shape, tuning it on first use."""
-    key = ("wgrad", _desc_tuple(d))
+    """(algo, ksplit) for this weight-gradient shape, tuning it on first use (pixel splits
+    capped at 16 for ops planned for a share of the chip)."""
+    key = _wgrad_key(d)
     hit = AUTOTUNE["cache"].get(key)
     if hit is not None:
         return hit
@@ -230,7 +250,7 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     torch.cuda.synchronize()
     for algo in range(1, 12):
         for ks in _WG_SPLITS:
-            if ks > nkt:
+            if ks > nkt or (ks > 16 and (d.flags & FLAG_CONCURRENT)):
                 break
             d.algo, d.ksplit = algo, ks
             ms = []
@@ -343,9 +363,10 @@ def _run_maybe_packed(fn_packed, fn_plain, d, pk):
     """Call with the packed image (desc flag set); fall back to packing inside the call
     when the tensors need a different plan (-21)."""
     if pk is not None:
-        d.flags = FLAG_WPACKED
+        base = d.flags
+        d.flags = base | FLAG_WPACKED
         rc = fn_packed()
-        d.flags = 0
+        d.flags = base
         if rc != -21:
             check(rc)
             return
@@ -517,7 +538,7 @@ def _conv_act_backward_fused(ctx, gy):
     wsp, wsn = (ws.data_ptr(), ws.numel()) if ws is not None else (None, 0)
     # the weight-gradient tile / split is autotuned on a shape's first call, which needs g:
     # that call runs the fused op without dW, tunes on its g, then runs the weight gradient
-    key = ("wgrad", _desc_tuple(d))
+    key = _wgrad_key(d)
     tune_first = (need_dw and AUTOTUNE["enabled"] and d.dtype == TPG_BF16 and key not in AUTOTUNE["cache"])
     if need_dw and not tune_first:
         d.algo, d.ksplit = AUTOTUNE["cache"].get(key, (0, 0))
