@@ -28,7 +28,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 / fp16 MFMA (MI355X_MICROARCH.md, chip table; fp32 mode: same denominator)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -37,19 +37,32 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--config", type=int, choices=[2, 3, 5], default=2,
+                    help="BASELINE.json configs[n-1]: 2 = full G+D step, 128x128, bs32, bf16 (the headline); "
+                         "3 = 2 + ResNet-50 identity loss; 5 = 256x256, bs16/GPU, fp16 MFMA, MobileNetV2 identity")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--img-size", type=int, default=None)
+    ap.add_argument("--dtype", choices=["bf16", "fp16", "fp32"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as hipGraph(s); off by default: on ROCm 7 the captured graph runs the "
                          "local-pathway side-stream branches serially (54.6 vs 47.1 ms/step measured)")
     ap.add_argument("--segmented", action="store_true", help="one hipGraph per step phase even at world 1")
     ap.add_argument("--probe-steps", type=int, default=2)
-    ap.add_argument("--identity", choices=["none", "resnet50", "mobilenetv2"], default="none",
+    ap.add_argument("--identity", choices=["none", "resnet50", "mobilenetv2"], default=None,
                     help="identity-preserving loss extractor in the G step (BASELINE configs[2]: resnet50)")
     ap.add_argument("--gp", action="store_true", help="WGAN-GP in the D step (double backward through D)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    dflt = {2: (32, 128, "bf16", "none"), 3: (32, 128, "bf16", "resnet50"), 5: (16, 256, "fp16", "mobilenetv2")}
+    b, im, dt, ident = dflt[a.config]
+    a.batch = a.batch or b
+    a.img_size = a.img_size or im
+    a.dtype = a.dtype or dt
+    a.identity = a.identity or ident
+    return a
 
 
 def main():
@@ -68,21 +81,23 @@ def main():
     import tpgan_train
     from config import G as GCFG
 
-    G = DG.Generator(GCFG["zdim"], GCFG["num_classes"], use_batchnorm=False).to(dev)
+    cdt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+    S = args.img_size
+    G = DG.Generator(GCFG["zdim"], GCFG["num_classes"], use_batchnorm=False, img_size=S).to(dev)
     D = DG.Discriminator().to(dev)
     identity_fn = None
     if args.identity != "none":
         import FeatureExtract as FE
         ext = FE.FeatureExtractModel(args.identity, 347).to(dev)
-        identity_fn = FE.IdentityPreservingLoss(ext, torch.bfloat16)
-    trainer = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16, identity_fn=identity_fn,
+        identity_fn = FE.IdentityPreservingLoss(ext, cdt)
+    trainer = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=cdt, identity_fn=identity_fn,
                                        gradient_penalty=args.gp)
     B = args.batch
-    batch = tpgan_train.synthetic_batch(B, dev, seed=1000 + rank)
+    batch = tpgan_train.synthetic_batch(B, dev, seed=1000 + rank, img_size=S)
 
-    # dominant kernel probe: enhance_features_128 (206 -> 206, 5x5, 128x128) forward
+    # dominant kernel probe: enhance_features_128 (206 -> 206, 5x5, at the full face size) forward
     def match(d, which):
-        return which == "fwd" and d.in_c == 206 and d.out_c == 206 and d.kh == 5 and d.in_h == 128
+        return which == "fwd" and d.in_c == 206 and d.out_c == 206 and d.kh == 5 and d.in_h == S
 
     # warm-up (autotunes the weight-gradient tiles), one eager step counted for the
     # algorithmic FLOPs, then the step is captured as hipGraph(s)
@@ -145,17 +160,27 @@ def main():
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
+        # the fixture-pinned CPU restatement (aten fp32) on the host cores, the
+        # headline workload (full step incl. both Adam updates) at its batch and BASELINE
+        # configs[0] at B=4, each one warm-up + median of --cpu-iters
         from oracle.cpu_step import time_cpu_step
-        fps, dt, thr = time_cpu_step(B=2, iters=args.cpu_iters, threads=args.cpu_threads)
-        cpu = {"value": round(fps, 4), "unit": "faces/s", "cores": thr, "kind": "port",
-               "sample": "oracle/cpu_step.py full G+D train step (no optimizer), B=2, %d timed steps after 1 warm-up, "
-                         "%.1f s/step, fp32 aten CPU" % (args.cpu_iters, dt)}
+        cb = min(B, args.cpu_batch) if args.img_size == 128 else 0
+        if cb:
+            r = time_cpu_step(B=cb, iters=args.cpu_iters, threads=args.cpu_threads)
+            cpu = {"value": round(r["full_fps"], 4), "unit": "faces/s", "cores": r["threads"], "kind": "port",
+                   "cpu_model": r["cpu"],
+                   "sample": "oracle/cpu_step.py full G+D train step incl. both Adam updates, 128x128, B=%d, fp32 "
+                             "aten CPU, 1 warm-up + median of %d steps (%.2f s/step)" % (cb, args.cpu_iters,
+                                                                                        r["full_s"]),
+                   "config1": {"value": round(r["config1_fps"], 4), "unit": "faces/s",
+                               "sample": "BASELINE configs[0]: global pathway + D fwd+bwd, B=4, median of %d "
+                                         "(%.2f s/step)" % (args.cpu_iters, r["config1_s"])}}
 
     # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
     # (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or null
     traffic, traffic_src = None, None
     pmc = os.path.join(REPO, "profiles", "pmc_dominant.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.config == 2 and S == 128 and args.dtype == "bf16" and B == 32:
         with open(pmc) as f:
             pj = json.load(f)
         traffic = int(pj["traffic_bytes"])
@@ -163,9 +188,16 @@ def main():
                        "dispatch of tools/bench_layers.py enhance_128 fwd; algorithmic %d B (x, residual in, y out, "
                        "weights)" % int(pj.get("algorithmic_bytes", 0)))
     workload = "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, 128x128, bf16"
-    if args.identity != "none":
+    ext_name = {"resnet50": "ResNet-50", "mobilenetv2": "MobileNetV2"}.get(args.identity)
+    if args.config == 5:
+        workload = ("BASELINE configs[4]: full two-pathway G + D train step, %dx%d, %s MFMA, %s identity-preserving "
+                    "loss, bs%d/GPU (G generalised to 256: LocalFuser placements and fc1 / deconv_8 sizes scale; "
+                    "parity unpinned at 256 for G)" % (S, S, args.dtype, ext_name or "no", B))
+    elif args.identity != "none":
         workload = ("BASELINE configs[2]: configs[1] + %s identity-preserving loss (frozen extractor, eval BN) "
-                    "in the G step" % {"resnet50": "ResNet-50", "mobilenetv2": "MobileNetV2"}[args.identity])
+                    "in the G step" % ext_name)
+    if args.config != 5 and (S != 128 or args.dtype != "bf16"):
+        workload += " [overridden: %dx%d, %s]" % (S, S, args.dtype)
     if args.gp:
         workload += " + WGAN-GP (double backward through D)"
     out = {
@@ -179,7 +211,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": args.dtype,
         "data": "synthetic (U[-1,1] Multi-PIE-shaped batch resident in HBM; random-init weights)",
         "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B,
                    "parallelism": "dp%d" % world,
@@ -188,8 +220,8 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "tpg halo_kernel fwd, enhance_features_128 (206->206, 5x5, 128x128, bs%d, +residual, "
-                               "LeakyReLU)" % B,
+                     "kernel": "tpg halo_kernel fwd, enhance_features_128 (206->206, 5x5, %dx%d, bs%d, +residual, "
+                               "LeakyReLU, %s)" % (S, S, B, args.dtype),
                      "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4), "launches": len(evs),
                      "timing": ("HIP events on the launch stream, eager probe steps after the timed graph replays"
                                 if graphed else "HIP events on the launch stream over the timed steps")},

@@ -57,14 +57,14 @@ extern "C" {
 
 typedef void* tpg_stream_t; /* hipStream_t */
 
-enum { TPG_F32 = 0, TPG_BF16 = 1 };
+enum { TPG_F32 = 0, TPG_BF16 = 1, TPG_F16 = 2 };
 enum { TPG_ACT_NONE = 0, TPG_ACT_RELU = 1, TPG_ACT_LEAKY = 2, TPG_ACT_RELU6 = 3 };
 enum { TPG_PAD_ZERO = 0, TPG_PAD_REFLECT = 1 };
 enum { TPG_OP_FWD = 0, TPG_OP_BWD_DATA = 1, TPG_OP_BWD_FILTER = 2 };
 
 typedef struct tpg_tensor {
   void* data;
-  int32_t dtype;      /* TPG_F32 / TPG_BF16 */
+  int32_t dtype;      /* TPG_F32 / TPG_BF16 / TPG_F16 */
   int32_t reserved;
   int64_t stride[4];  /* element strides of the logical (n, c, h, w) view */
 } tpg_tensor;
@@ -78,7 +78,8 @@ typedef struct tpg_conv_desc {
   int32_t pad_t, pad_b, pad_l, pad_r;
   int32_t pad_mode;               /* TPG_PAD_*; reflect only for transposed == 0 */
   int32_t transposed;             /* 0: Conv2d, 1: ConvTranspose2d (output_padding = out - natural) */
-  int32_t dtype;                  /* activation / arithmetic dtype, TPG_F32 or TPG_BF16 */
+  int32_t dtype;                  /* activation / arithmetic dtype: TPG_F32 (exact fp32 MFMA), TPG_BF16 or
+                                     TPG_F16 (16-bit MFMA operands, fp32 accumulate) */
   int32_t act;                    /* TPG_ACT_* applied after bias (+ residual) */
   float slope;                    /* LeakyReLU negative slope */
   float res_scale;                /* ResidualBlock scaling_factor (ModificationLayer.py:300) */

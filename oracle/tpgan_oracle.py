@@ -85,11 +85,25 @@ FUSER_PADS = (
 )
 
 
+def fuser_pads(img_size=128):
+    """FUSER_PADS at 128; at k*128 (build extension for BASELINE configs[4], no reference
+    counterpart) the landmark centres and patch sizes scale by k, placement centre - half - 1."""
+    if img_size == 128:
+        return FUSER_PADS
+    k = img_size // 128
+    out = []
+    for (cx, cy), (h, w) in zip(((39, 40), (86, 39), (64, 64), (65, 89)), ((40, 40), (40, 40), (32, 40), (32, 48))):
+        top, left = cy * k - h * k // 2 - 1, cx * k - w * k // 2 - 1
+        out.append((left, img_size - left - w * k, top, img_size - top - h * k))
+    return tuple(out)
+
+
 def local_fuser(le, re, nose, mouth):
     """LocalFuser.forward (D_and_G_model.py:132-159): zero-pad to 128x128, max over the
     stack (first index wins ties, so padding zeros of an earlier patch win over a
-    negative value of a later one)."""
-    xs = [F.pad(t, p) for t, p in zip((le, re, nose, mouth), FUSER_PADS)]
+    negative value of a later one).  The canvas is 128 * (eye height / 40)."""
+    pads = fuser_pads(128 * le.shape[2] // 40)
+    xs = [F.pad(t, p) for t, p in zip((le, re, nose, mouth), pads)]
     return torch.max(torch.stack(xs, 0), 0)[0]
 
 
@@ -189,10 +203,16 @@ def g_param_shapes():
     return keys["G"], keys["D"]
 
 
-def make_params(dtype=torch.float64, seed=0):
-    """Deterministic G and D parameter dicts (oracle.det_init)."""
+def make_params(dtype=torch.float64, seed=0, img_size=128):
+    """Deterministic G and D parameter dicts (oracle.det_init).  img_size 256: fc1 takes
+    512*16*16 inputs and deconv_8 has a 16x16 kernel (build extension, BASELINE configs[4])."""
     from .det_init import det_param
     gk, dk = g_param_shapes()
+    if img_size != 128:
+        e = img_size // 16
+        fix = {"global_pathway.fc1.weight": [512, 512 * e * e],
+               "global_pathway.deconv_8.0.weight": [320, 64, e, e]}
+        gk = [(k, fix.get(k, s)) for k, s in gk]
     PG = {k: torch.from_numpy(det_param("G/" + k, s, seed)).to(dtype) for k, s in gk}
     PD = {k: torch.from_numpy(det_param("D/" + k, s, seed)).to(dtype) for k, s in dk}
     return PG, PD

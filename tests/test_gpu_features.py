@@ -111,8 +111,10 @@ def _mnv2_oracle_dx_floor(G):
     return rel(x.grad.double(), G["train:dx"])
 
 
-def test_mobilenet_v2_bf16_eval(gpu):
-    G, m, x, outs, tag = _mnv2_run(gpu, False, torch.bfloat16)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def test_mobilenet_v2_bf16_eval(gpu, dtype):
+    """16-bit MFMA / depthwise paths (bf16; fp16 = BASELINE configs[4]'s extractor dtype)."""
+    G, m, x, outs, tag = _mnv2_run(gpu, False, dtype)
     for k, v in outs.items():
         assert rel(v.detach().float().cpu(), G["eval:%s" % k]) < 3e-2, k
     # the input gradient crosses 52 bf16 layers (each rounding activations and gradients
@@ -217,7 +219,7 @@ def test_dwconv_vs_aten(gpu, c, h, w, stride, dtype):
     assert rel(bg.grad.cpu(), br.grad) < tol * 4
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_maxpool_avgpool_vs_aten(gpu, dtype):
     import tpgan_ops
     g = torch.Generator().manual_seed(7)

@@ -319,3 +319,40 @@ def test_bs32_step_properties(gpu):
         err2, err32 = rel(c2[i], a2[i]), rel(c[i], a[i])
         shrink = float(a2[i].norm()) / float(a[i].norm())
         assert err32 < max(5e-2, 3 * err2 * shrink), (tag, err32, err2, shrink)
+
+
+def test_config5_fp16_256_step(gpu):
+    """BASELINE configs[4] in small: the 256x256 G + D train step in fp16 (static loss scale,
+    unscaled in the Adam launch) with the MobileNetV2 identity loss, B=2: finite losses,
+    parameters and gradients; the fp16 step's gradients against the fp32 step's from the same
+    weights and batch, within the bf16-style bound of test_bs32_step_properties."""
+    import D_and_G_model as DG
+    import FeatureExtract as FE
+    import tpgan_ops
+    import tpgan_train
+    from _cases import load_det
+    res = {}
+    for dt in (torch.float32, torch.float16):
+        G = DG.Generator(64, 347, use_batchnorm=False, img_size=256)
+        D = DG.Discriminator()
+        load_det(G, "G/", torch.float32)
+        load_det(D, "D/", torch.float32)
+        G, D = G.to(gpu), D.to(gpu)
+        torch.manual_seed(0)
+        ext = FE.FeatureExtractModel("mobilenetv2", 347).to(gpu)
+        tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=dt, use_dropout=False,
+                                      identity_fn=FE.IdentityPreservingLoss(ext, dt))
+        assert tr.loss_scale == (1024.0 if dt == torch.float16 else 1.0)
+        b = tpgan_train.synthetic_batch(2, gpu, seed=31, img_size=256)
+        with tpgan_ops.deterministic(dt == torch.float32):
+            out = tr.step(b)
+            torch.cuda.synchronize()
+        assert np.isfinite(float(out["loss_D"])) and np.isfinite(float(out["loss_G"])), dt
+        for f in (tr.fG, tr.fD):
+            assert bool(torch.isfinite(f.grad).all()) and bool(torch.isfinite(f.data).all()), dt
+        res[dt] = (float(out["loss_G"]), (tr.fG.grad / tr.loss_scale).cpu(), (tr.fD.grad / tr.loss_scale).cpu())
+        del tr, G, D, ext
+        torch.cuda.empty_cache()
+    a, c = res[torch.float32], res[torch.float16]
+    assert abs(c[0] - a[0]) <= 2e-2 * abs(a[0])
+    assert rel(c[1], a[1]) < 1e-1 and rel(c[2], a[2]) < 1e-1, (rel(c[1], a[1]), rel(c[2], a[2]))

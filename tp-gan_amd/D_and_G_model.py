@@ -71,19 +71,33 @@ class LocalPathway(nn.Module):
 class LocalFuser(nn.Module):
     """Zero-pad the four parts onto a 128x128 canvas and take the element-wise max
     (D_and_G_model.py:112-159).  Placements (top, left) follow the reference's pad
-    arithmetic (:154-157); ties resolve to the first part, as torch.max does."""
+    arithmetic (:154-157); ties resolve to the first part, as torch.max does.
+
+    img_size (build extension, BASELINE configs[4]; the reference is 128-only, :152): the
+    patch sizes and the landmark centres of the 128 canvas scale by img_size / 128, and the
+    placement keeps the reference's form centre - half - 1."""
 
     EYE_WIDTH, EYE_HEIGHT = 40, 40
     NOSE_WIDTH, NOSE_HEIGHT = 40, 32
     MOUTH_WIDTH, MOUTH_HEIGHT = 48, 32
     IMG_SIZE = 128
+    # landmark centres (x, y) of the 128 canvas: left eye, right eye, nose, mouth (:154-157)
+    CENTERS = ((39, 40), (86, 39), (64, 64), (65, 89))
     # (top, left) of left eye, right eye, nose, mouth
     TOPS = (40 - 20 - 1, 39 - 20 - 1, 64 - 16 - 1, 89 - 16 - 1)
     LEFTS = (39 - 20 - 1, 86 - 20 - 1, 64 - 20 - 1, 65 - 24 - 1)
     SIZES = ((40, 40), (40, 40), (32, 40), (32, 48))
 
-    def __init__(self):
+    def __init__(self, img_size=128):
         super(LocalFuser, self).__init__()
+        if img_size % 128:
+            raise ValueError("LocalFuser: img_size must be a multiple of 128, got %d" % img_size)
+        if img_size != 128:
+            k = img_size // 128
+            self.IMG_SIZE = img_size
+            self.SIZES = tuple((h * k, w * k) for h, w in LocalFuser.SIZES)
+            self.TOPS = tuple(cy * k - h * k // 2 - 1 for (cx, cy), (h, w) in zip(self.CENTERS, LocalFuser.SIZES))
+            self.LEFTS = tuple(cx * k - w * k // 2 - 1 for (cx, cy), (h, w) in zip(self.CENTERS, LocalFuser.SIZES))
 
     def forward(self, f_left_eye, f_right_eye, f_nose, f_mouth):
         parts = (f_left_eye, f_right_eye, f_nose, f_mouth)
@@ -97,8 +111,13 @@ class GlobalPathway(nn.Module):
     """Global encoder-decoder over the 128x128 face (D_and_G_model.py:161-329), R3 applied."""
 
     def __init__(self, zdim, local_feature_layer_dim=64, use_batchnorm=True, use_residual_block=True,
-                 scaling_factor=1.0, FM_multiplier=1.0):
+                 scaling_factor=1.0, FM_multiplier=1.0, img_size=128):
         super(GlobalPathway, self).__init__()
+        # img_size (build extension, BASELINE configs[4]): the encoder ends at img_size / 16;
+        # fc1 (:212, 512*8*8 inputs at 128) and the deconv_8 kernel (:218, 8 = the 8x8 map it
+        # must produce) follow that size
+        self.img_size = img_size
+        e = img_size // 16
         n_FM_encoder = EMaC2I([64, 64, 128, 256, 512], FM_multiplier)
         n_FM_decoder = EMaC2I([64, 32, 16, 8], FM_multiplier)
         n_FM_decoder_enhance_features = EMaC2I([512, 256, 128, 64], FM_multiplier)
@@ -119,9 +138,9 @@ class GlobalPathway(nn.Module):
         self.conv4 = sequential(conv(n_FM_encoder[3], n_FM_encoder[4], 3, 2, 1, "kaiming", L(1e-2), use_batchnorm),
                                 *[ResidualBlock(512, 512, 3, 1, 1, "kaiming", L(1e-2), is_bottleneck=False,
                                                 scaling_factor=sf) for i in range(4)])
-        self.fc1 = nn.Linear(n_FM_encoder[4] * 8 * 8, 512)
+        self.fc1 = nn.Linear(n_FM_encoder[4] * e * e, 512)
         self.fc2 = nn.MaxPool1d(2, 2, 0)
-        self.deconv_8 = deconv(256 + self.zdim, n_FM_decoder[0], 8, 1, 0, 0, "kaiming", nn.ReLU(), use_batchnorm)
+        self.deconv_8 = deconv(256 + self.zdim, n_FM_decoder[0], e, 1, 0, 0, "kaiming", nn.ReLU(), use_batchnorm)
         self.deconv_32 = deconv(n_FM_decoder[0], n_FM_decoder[1], 3, 4, 0, 1, "kaiming", nn.ReLU(), use_batchnorm)
         self.deconv_64 = deconv(n_FM_decoder[1], n_FM_decoder[2], 3, 2, 1, 1, "kaiming", nn.ReLU(), use_batchnorm)
         self.deconv_128 = deconv(n_FM_decoder[2], n_FM_decoder[3], 3, 2, 1, 1, "kaiming", nn.ReLU(), use_batchnorm)
@@ -187,11 +206,11 @@ class GlobalPathway(nn.Module):
         deconv_128 = self.deconv_128(deconv_64)
         add_conv_and_deconv_8 = self.add_conv_and_deconv_8(cat([deconv_8, conv4]))
         enhance_features_8 = self.enhance_features_8(add_conv_and_deconv_8)
-        assert enhance_features_8.shape[2] == 8
+        assert enhance_features_8.shape[2] == self.img_size // 16  # :301
         upsample_16 = self.upsample_16(enhance_features_8)
         add_conv_and_deconv_16 = self.add_conv_and_deconv_16(conv3)
         enhance_features_16 = self.enhance_features_16(cat([upsample_16, add_conv_and_deconv_16]))
-        assert enhance_features_16.shape[2] == 16
+        assert enhance_features_16.shape[2] == self.img_size // 8  # :308
         upsample_32 = self.upsample_32(enhance_features_16)
         add_conv_and_deconv_32 = self.add_conv_and_deconv_32(cat([deconv_32, conv2]))
         enhance_features_32 = self.enhance_features_32(cat([upsample_32, add_conv_and_deconv_32]))
@@ -232,14 +251,16 @@ class Generator(nn.Module):
     """Four LocalPathways, three LocalFuser calls, the GlobalPathway and FeaturePredict;
     forward returns the reference's 8-tuple (D_and_G_model.py:350-407)."""
 
-    def __init__(self, zdim, num_classes, use_batchnorm=True, use_residual_block=True):
+    def __init__(self, zdim, num_classes, use_batchnorm=True, use_residual_block=True, img_size=128):
         super(Generator, self).__init__()
+        self.img_size = img_size  # build extension (BASELINE configs[4]: 256); the reference is 128-only
         self.local_pathway_left_eye = LocalPathway(use_batchnorm=use_batchnorm)
         self.local_pathway_right_eye = LocalPathway(use_batchnorm=use_batchnorm)
         self.local_pathway_nose = LocalPathway(use_batchnorm=use_batchnorm)
         self.local_pathway_mouth = LocalPathway(use_batchnorm=use_batchnorm)
-        self.global_pathway = GlobalPathway(zdim, use_batchnorm=use_batchnorm, use_residual_block=use_residual_block)
-        self.local_fuser = LocalFuser()
+        self.global_pathway = GlobalPathway(zdim, use_batchnorm=use_batchnorm, use_residual_block=use_residual_block,
+                                            img_size=img_size)
+        self.local_fuser = LocalFuser(img_size)
         self.feature_predict = FeaturePredict(num_classes)
 
     def forward(self, I128, left_eye, right_eye, nose, mouth, z, use_dropout):

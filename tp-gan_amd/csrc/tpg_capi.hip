@@ -75,7 +75,8 @@ static int32_t hip_check(int e, const char* what) {
   return fail(e > 0 ? e : -100, "%s failed: %s", what, e > 0 ? hipGetErrorString((hipError_t)e) : "bad config");
 }
 
-static inline int esize(int dtype) { return dtype == TPG_BF16 ? 2 : 4; }
+static inline int esize(int dtype) { return dtype == TPG_F32 ? 4 : 2; }
+static inline bool half16(int dtype) { return dtype == TPG_BF16 || dtype == TPG_F16; }  // 16-bit MFMA operands
 static inline int64_t rup(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 static inline int pmod(int a, int m) { return ((a % m) + m) % m; }
@@ -105,7 +106,7 @@ static int choose_cfg(int nout) {
 // fill unit / tile / split-K bookkeeping once geometry, C, Nout and taps are known
 static void finish(Prob& P, int dtype, int M) {
   IgemmArgs& a = P.a;
-  const int upk = dtype == TPG_BF16 ? 4 : 2;
+  const int upk = half16(dtype) ? 4 : 2;
   a.upt = cdiv(std::max(a.C, 1), 16);
   a.nunits = a.ntaps > 0 ? (int)rup((int64_t)a.ntaps * a.upt, upk) : 0;
   a.M = M;
@@ -197,12 +198,24 @@ static bool vec_ok(const tpg_tensor& t, int dtype) {
   return true;
 }
 
+// geometry of a full-kernel conv (kernel = input map, 1x1 output) or a transposed conv of a
+// 1x1 map (output = kernel), no padding: the composite-channel GEMM forms
+static bool gemm_form(const tpg_conv_desc* d) {
+  if (d->pad_t || d->pad_b || d->pad_l || d->pad_r || d->pad_mode) return false;
+  if (!d->transposed) return d->in_h == d->kh && d->in_w == d->kw && d->out_h == 1 && d->out_w == 1;
+  return d->in_h == 1 && d->in_w == 1 && d->out_h == d->kh && d->out_w == d->kw;
+}
+static bool big_taps(const tpg_conv_desc* d) { return d->kh * d->kw > TPG_MAX_TAPS; }
+
 static int32_t check_desc(const tpg_conv_desc* d) {
   if (!d) return fail(-1, "null descriptor");
   if (d->n <= 0 || d->in_c <= 0 || d->out_c <= 0 || d->kh <= 0 || d->kw <= 0) return fail(-2, "bad sizes");
   if (d->stride_h <= 0 || d->stride_w <= 0) return fail(-2, "bad stride");
-  if (d->dtype != TPG_F32 && d->dtype != TPG_BF16) return fail(-3, "bad dtype %d", d->dtype);
-  if (d->kh * d->kw > TPG_MAX_TAPS) return fail(-4, "kernel %dx%d has more than %d taps", d->kh, d->kw, TPG_MAX_TAPS);
+  if (d->dtype != TPG_F32 && d->dtype != TPG_BF16 && d->dtype != TPG_F16) return fail(-3, "bad dtype %d", d->dtype);
+  // more taps than the tap tables hold: only the full-kernel GEMM forms (fc1 / deconv_8 at
+  // 256x256: 16x16 kernels on a 16x16 map or from a 1x1 map), which need no tap table
+  if (d->kh * d->kw > TPG_MAX_TAPS && !gemm_form(d))
+    return fail(-4, "kernel %dx%d has more than %d taps", d->kh, d->kw, TPG_MAX_TAPS);
   if (d->transposed) {
     if (d->pad_mode != TPG_PAD_ZERO) return fail(-5, "reflect padding is only defined for Conv2d");
     int nh = (d->in_h - 1) * d->stride_h - d->pad_t - d->pad_b + d->kh;
@@ -283,7 +296,7 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   if (cfg < 0) return;
   HaloArgs& h = P.h;
   memset(&h, 0, sizeof(h));
-  const int ks_elems = dtype == TPG_BF16 ? 32 : 16;
+  const int ks_elems = half16(dtype) ? 32 : 16;
   h.A_H = a.A_H; h.A_W = a.A_W; h.C = a.C;
   h.nks = cdiv(a.C, ks_elems);
   h.ntaps = a.ntaps;
@@ -452,12 +465,12 @@ extern "C" size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op) {
   ShareScope share_scope(d);
   if (check_desc(d)) return 0;
   if (op == TPG_OP_FWD) {
-    size_t a = probs_ws(plan_fwd(d, false));
+    size_t a = big_taps(d) ? 0 : probs_ws(plan_fwd(d, false));
     if (fwd_composite(d, nullptr, nullptr)) a = std::max(a, probs_ws(plan_fwd(d, true)));
     return a + 256;
   }
   if (op == TPG_OP_BWD_DATA) {
-    size_t a = probs_ws(plan_bwd_data(d, false)) + reflect_tmp_bytes(d);
+    size_t a = big_taps(d) ? 0 : probs_ws(plan_bwd_data(d, false)) + reflect_tmp_bytes(d);
     if (bwd_data_composite(d, nullptr, nullptr)) a = std::max(a, probs_ws(plan_bwd_data(d, true)));
     return a + 256;
   }
@@ -678,6 +691,7 @@ extern "C" int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   if (residual.data && (rc = check_tensor(residual, d->dtype, "residual"))) return rc;
   const bool comp = fwd_composite(d, &x, &y);
   const bool packed = d->flags & TPG_FLAG_WPACKED;
+  if (!comp && big_taps(d)) return fail(-4, "%dx%d kernel: only the dense NHWC GEMM form is supported", d->kh, d->kw);
   if (packed && comp != fwd_composite(d, nullptr, nullptr))
     return fail(-21, "pre-packed weights assume a full-kernel GEMM; these tensors are not dense NHWC");
   std::vector<Prob> v = plan_fwd(d, comp);
@@ -698,6 +712,7 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
   if (!w.data || (w.dtype != TPG_F32 && !packed)) return fail(-13, "weight must be fp32");
   hipStream_t s = (hipStream_t)stream;
   const bool comp = bwd_data_composite(d, &g, &dx);
+  if (!comp && big_taps(d)) return fail(-4, "%dx%d kernel: only the dense NHWC GEMM form is supported", d->kh, d->kw);
   if (packed && comp != bwd_data_composite(d, nullptr, nullptr))
     return fail(-21, "pre-packed weights assume a full-kernel GEMM; these tensors are not dense NHWC");
   const char* pk = packed ? reinterpret_cast<const char*>(w.data) : nullptr;
@@ -727,7 +742,7 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
 // shape is not covered (caller falls back), else the launch status.
 static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_tensor& g, const tpg_tensor& dw,
                         float* dbias, hipStream_t stream) {
-  if (d->dtype != TPG_BF16 || d->stride_h != 1 || d->stride_w != 1) return 1;
+  if (!half16(d->dtype) || d->stride_h != 1 || d->stride_w != 1) return 1;
   const int PH = d->out_h, PW = d->out_w, QH = d->in_h, QW = d->in_w;
   // row mode: one kernel row, 3/5/7 taps, 64-pixel row segments; image mode (algos 10, 11 and
   // the default below 64 pixels of width): all taps of a 2x2 / 3x3 kernel from one halo of
@@ -752,6 +767,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   if (pb >= (1ll << 31) || qb >= (1ll << 31)) return 1;
   WgradRHArgs a;
   memset(&a, 0, sizeof(a));
+  a.dtype = d->dtype;
   a.P = g.data; a.p_sn = (int)g.stride[0]; a.p_sh = (int)g.stride[2]; a.p_sw = (int)g.stride[3];
   a.PH = PH; a.PW = PW; a.Ca = d->out_c; a.p_bytes = (int)pb;
   a.Q = x.data; a.q_sn = (int)x.stride[0]; a.q_sh = (int)x.stride[2]; a.q_sw = (int)x.stride[3];
@@ -828,6 +844,7 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
   const int QH = d->transposed ? d->out_h : d->in_h, QW = d->transposed ? d->out_w : d->in_w;
   const int Ca = d->transposed ? d->in_c : d->out_c, cb = d->transposed ? d->out_c : d->in_c;
   const bool comp = d->transposed ? bwd_data_composite(d, &g, nullptr) : fwd_composite(d, &x, nullptr);
+  if (!comp && big_taps(d)) return fail(-4, "%dx%d kernel: only the dense NHWC GEMM form is supported", d->kh, d->kw);
   a.P = P.data; a.p_sn = P.stride[0]; a.p_sh = P.stride[2]; a.p_sw = P.stride[3];
   a.Q = Q.data; a.q_sn = Q.stride[0]; a.q_sh = Q.stride[2]; a.q_sw = Q.stride[3];
   a.Ca = Ca;
@@ -880,7 +897,7 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
     // lower operand reuse; about 2048 blocks).  Callers that autotune pass their choice in
     // the descriptor: algo = tile index + 1 into cand[], ksplit = pixel splits.
     static const int cand[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
-    const int kp = d->dtype == TPG_BF16 ? 64 : 32;
+    const int kp = half16(d->dtype) ? 64 : 32;
     const int nkt = cdiv(a.npix, kp);
     int bm = 0, bn = 0, bks = 1;
     {

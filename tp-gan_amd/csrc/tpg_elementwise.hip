@@ -9,10 +9,13 @@
 namespace tpg {
 
 __device__ __forceinline__ float ld_any(const void* p, int dtype, int64_t off) {
-  return dtype == TPG_BF16 ? (float)reinterpret_cast<const __bf16*>(p)[off] : reinterpret_cast<const float*>(p)[off];
+  return dtype == TPG_BF16 ? (float)reinterpret_cast<const __bf16*>(p)[off]
+       : dtype == TPG_F16  ? (float)reinterpret_cast<const _Float16*>(p)[off]
+                           : reinterpret_cast<const float*>(p)[off];
 }
 __device__ __forceinline__ void st_any(void* p, int dtype, int64_t off, float v) {
   if (dtype == TPG_BF16) reinterpret_cast<__bf16*>(p)[off] = (__bf16)v;
+  else if (dtype == TPG_F16) reinterpret_cast<_Float16*>(p)[off] = (_Float16)v;
   else reinterpret_cast<float*>(p)[off] = v;
 }
 
@@ -56,9 +59,11 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restric
   if (idx >= job.items) return;
   if (job.kind == 1) {
     if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx);
+    else if (job.k.dtype == TPG_F16) pack_halo_item<_Float16>(job.k, job.bn, job.bnl, job.ntiles, idx);
     else pack_halo_item<float>(job.k, job.bn, job.bnl, job.ntiles, idx);
   } else {
     if (job.k.dtype == TPG_BF16) pack_igemm_item<__bf16>(job.k, idx);
+    else if (job.k.dtype == TPG_F16) pack_igemm_item<_Float16>(job.k, idx);
     else pack_igemm_item<float>(job.k, idx);
   }
 }
@@ -73,6 +78,7 @@ int launch_pack(const PackArgs& a, hipStream_t s) {
   const int nthreads = a.Npad * a.nunits;
   const int blocks = (nthreads + 255) / 256;
   if (a.dtype == TPG_BF16) hipLaunchKernelGGL(pack_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a, nthreads);
+  else if (a.dtype == TPG_F16) hipLaunchKernelGGL(pack_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, a, nthreads);
   else hipLaunchKernelGGL(pack_kernel<float>, dim3(blocks), dim3(256), 0, s, a, nthreads);
   return (int)hipGetLastError();
 }
@@ -449,7 +455,7 @@ static int act_cap() {
 
 
 static bool pix_dense_vec(const tpg_tensor& t, int h, int w, int dtype, int c) {
-  const int es = dtype == TPG_BF16 ? 2 : 4, epc = 16 / es;
+  const int es = dtype != TPG_F32 ? 2 : 4, epc = 16 / es;
   if (t.dtype != dtype || t.stride[1] != 1) return false;
   const int64_t ps = t.stride[3];
   if (ps % epc || ps < (c + epc - 1) / epc * epc) return false;
@@ -460,7 +466,7 @@ static bool pix_dense_vec(const tpg_tensor& t, int h, int w, int dtype, int c) {
 extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
                                      tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, hipStream_t s) {
   const int dt = g.dtype;
-  const int epc = dt == TPG_BF16 ? 8 : 4;
+  const int epc = dt != TPG_F32 ? 8 : 4;
   static const bool force_scalar = getenv("TPG_ACTB_SCALAR") != nullptr;  // debug switch
   if (!force_scalar && c <= 1024 && (c + epc - 1) / epc <= 256 && pix_dense_vec(gy, h, w, dt, c) && pix_dense_vec(g, h, w, dt, c) &&
       (act == TPG_ACT_NONE || pix_dense_vec(y, h, w, dt, c))) {
@@ -473,7 +479,11 @@ extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, 
     const int64_t blocks = (dbias && deterministic()) ? 1 :
         std::max<int64_t>(1, std::min<int64_t>((npix + act_ppl() * ppi - 1) / (act_ppl() * ppi), act_cap()));
     const int64_t ppb = (npix + blocks - 1) / blocks;
-    if (dt == TPG_BF16)
+    if (dt == TPG_F16)
+      hipLaunchKernelGGL(act_bwd_vec_kernel<_Float16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
+                         (const _Float16*)gy.data, gy.stride[3], (const _Float16*)y.data, y.stride[3], (_Float16*)g.data,
+                         g.stride[3], dbias, ppb);
+    else if (dt == TPG_BF16)
       hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
                          (const __bf16*)gy.data, gy.stride[3], (const __bf16*)y.data, y.stride[3], (__bf16*)g.data,
                          g.stride[3], dbias, ppb);

@@ -516,7 +516,7 @@ inline int grid_cap(int64_t total, int cap = 8192) {
 }
 
 bool chunk_ok(const tpg_tensor& t, int C) {
-  const int es = t.dtype == TPG_BF16 ? 2 : 4, epc = 16 / es;
+  const int es = t.dtype != TPG_F32 ? 2 : 4, epc = 16 / es;
   if (t.stride[1] != 1 || ((uintptr_t)t.data) % 16) return false;
   for (int i : {0, 2, 3})
     if (t.stride[i] % epc) return false;
@@ -528,7 +528,7 @@ int dw_check(const tpg_conv_desc* d) {
   if (d->in_c != d->out_c || d->transposed || d->pad_mode != TPG_PAD_ZERO)
     return ffail(-2, "depthwise: in_c must equal out_c, zero padding, no transposition");
   if (d->kh * d->kw > 9 || d->kh < 1 || d->kw < 1) return ffail(-4, "depthwise: kernels up to 3x3");
-  if (d->dtype != TPG_F32 && d->dtype != TPG_BF16) return ffail(-3, "bad dtype");
+  if (d->dtype != TPG_F32 && d->dtype != TPG_BF16 && d->dtype != TPG_F16) return ffail(-3, "bad dtype");
   const int oh = (d->in_h + d->pad_t + d->pad_b - d->kh) / d->stride_h + 1;
   const int ow = (d->in_w + d->pad_l + d->pad_r - d->kw) / d->stride_w + 1;
   if (oh != d->out_h || ow != d->out_w) return ffail(-6, "depthwise: output size inconsistent with geometry");
@@ -573,7 +573,10 @@ extern "C" int32_t tpg_dwconv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_te
   a.r_sn = residual.stride[0]; a.r_sh = residual.stride[2]; a.r_sw = residual.stride[3];
   const dim3 grid = dw_grid(a, (int64_t)a.N * a.OH * a.OW, 4, 4096);
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == TPG_BF16)
+  if (d->dtype == TPG_F16)
+    hipLaunchKernelGGL(dw_fwd_kernel<_Float16>, grid, dim3(256), 0, s, a, (const _Float16*)x.data, (_Float16*)y.data,
+                       (const _Float16*)residual.data);
+  else if (d->dtype == TPG_BF16)
     hipLaunchKernelGGL(dw_fwd_kernel<__bf16>, grid, dim3(256), 0, s, a, (const __bf16*)x.data, (__bf16*)y.data,
                        (const __bf16*)residual.data);
   else
@@ -591,7 +594,9 @@ extern "C" int32_t tpg_dwconv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, t
   DwArgs a = dw_args(d, dx, g, w);
   const dim3 grid = dw_grid(a, (int64_t)a.N * a.H * a.W, 4, 4096);
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == TPG_BF16)
+  if (d->dtype == TPG_F16)
+    hipLaunchKernelGGL(dw_dgrad_kernel<_Float16>, grid, dim3(256), 0, s, a, (const _Float16*)g.data, (_Float16*)dx.data);
+  else if (d->dtype == TPG_BF16)
     hipLaunchKernelGGL(dw_dgrad_kernel<__bf16>, grid, dim3(256), 0, s, a, (const __bf16*)g.data, (__bf16*)dx.data);
   else
     hipLaunchKernelGGL(dw_dgrad_kernel<float>, grid, dim3(256), 0, s, a, (const float*)g.data, (float*)dx.data);
@@ -608,7 +613,10 @@ extern "C" int32_t tpg_dwconv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x,
   a.w = nullptr;
   const dim3 grid = dw_grid(a, (int64_t)a.N * a.OH * a.OW, 16, 256);
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == TPG_BF16)
+  if (d->dtype == TPG_F16)
+    hipLaunchKernelGGL(dw_wgrad_kernel<_Float16>, grid, dim3(256), 0, s, a, (const _Float16*)x.data,
+                       (const _Float16*)g.data, (float*)dw.data);
+  else if (d->dtype == TPG_BF16)
     hipLaunchKernelGGL(dw_wgrad_kernel<__bf16>, grid, dim3(256), 0, s, a, (const __bf16*)x.data,
                        (const __bf16*)g.data, (float*)dw.data);
   else
@@ -626,7 +634,11 @@ extern "C" int32_t tpg_maxpool2d_fwd(int32_t n, int32_t c, int32_t h, int32_t w,
   if (x.dtype != y.dtype || x.stride[1] != 1 || y.stride[1] != 1) return ffail(-12, "maxpool: channels-last, one dtype");
   hipStream_t st = (hipStream_t)stream;
   const int grid = grid_cap((int64_t)n * oh * ow * c);
-  if (x.dtype == TPG_BF16)
+  if (x.dtype == TPG_F16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<_Float16>, dim3(grid), dim3(256), 0, st, n, c, h, w, oh, ow, k, s, p,
+                       (const _Float16*)x.data, x.stride[0], x.stride[2], x.stride[3], (_Float16*)y.data, y.stride[0],
+                       y.stride[2], y.stride[3], argmax);
+  else if (x.dtype == TPG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, n, c, h, w, oh, ow, k, s, p,
                        (const __bf16*)x.data, x.stride[0], x.stride[2], x.stride[3], (__bf16*)y.data, y.stride[0],
                        y.stride[2], y.stride[3], argmax);
@@ -645,7 +657,11 @@ extern "C" int32_t tpg_maxpool2d_bwd(int32_t n, int32_t c, int32_t h, int32_t w,
   if (gy.dtype != dx.dtype || gy.stride[1] != 1 || dx.stride[1] != 1) return ffail(-12, "maxpool: channels-last");
   hipStream_t st = (hipStream_t)stream;
   const int grid = grid_cap((int64_t)n * h * w * c);
-  if (gy.dtype == TPG_BF16)
+  if (gy.dtype == TPG_F16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<_Float16>, dim3(grid), dim3(256), 0, st, n, c, h, w, oh, ow, k, s, p,
+                       (const _Float16*)gy.data, gy.stride[0], gy.stride[2], gy.stride[3], argmax, (_Float16*)dx.data,
+                       dx.stride[0], dx.stride[2], dx.stride[3]);
+  else if (gy.dtype == TPG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, n, c, h, w, oh, ow, k, s, p,
                        (const __bf16*)gy.data, gy.stride[0], gy.stride[2], gy.stride[3], argmax, (__bf16*)dx.data,
                        dx.stride[0], dx.stride[2], dx.stride[3]);
@@ -662,7 +678,10 @@ extern "C" int32_t tpg_avgpool_fwd(int32_t n, int32_t c, int32_t h, int32_t w, t
   if (x.dtype != y.dtype || x.stride[1] != 1 || y.stride[1] != 1) return ffail(-12, "avgpool: channels-last");
   hipStream_t st = (hipStream_t)stream;
   const int grid = (n * c + 255) / 256;
-  if (x.dtype == TPG_BF16)
+  if (x.dtype == TPG_F16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<_Float16>, dim3(grid), dim3(256), 0, st, n, c, h, w, (const _Float16*)x.data,
+                       x.stride[0], x.stride[2], x.stride[3], (_Float16*)y.data, y.stride[0]);
+  else if (x.dtype == TPG_BF16)
     hipLaunchKernelGGL(avgpool_fwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, n, c, h, w, (const __bf16*)x.data,
                        x.stride[0], x.stride[2], x.stride[3], (__bf16*)y.data, y.stride[0]);
   else
@@ -677,7 +696,10 @@ extern "C" int32_t tpg_avgpool_bwd(int32_t n, int32_t c, int32_t h, int32_t w, t
   if (gy.dtype != dx.dtype || gy.stride[1] != 1 || dx.stride[1] != 1) return ffail(-12, "avgpool: channels-last");
   hipStream_t st = (hipStream_t)stream;
   const int grid = grid_cap((int64_t)n * h * w * c);
-  if (gy.dtype == TPG_BF16)
+  if (gy.dtype == TPG_F16)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<_Float16>, dim3(grid), dim3(256), 0, st, n, c, h, w, (const _Float16*)gy.data,
+                       gy.stride[0], (_Float16*)dx.data, dx.stride[0], dx.stride[2], dx.stride[3]);
+  else if (gy.dtype == TPG_BF16)
     hipLaunchKernelGGL(avgpool_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, n, c, h, w, (const __bf16*)gy.data,
                        gy.stride[0], (__bf16*)dx.data, dx.stride[0], dx.stride[2], dx.stride[3]);
   else
@@ -701,7 +723,7 @@ extern "C" int32_t tpg_bn_fold(int32_t cout, int32_t cin, int32_t kh, int32_t kw
 namespace {
 
 bool pix_dense(const tpg_tensor& t, int h, int w, int C, int dtype) {
-  const int es = dtype == TPG_BF16 ? 2 : 4, epc = 16 / es;
+  const int es = dtype != TPG_F32 ? 2 : 4, epc = 16 / es;
   if (t.dtype != dtype || t.stride[1] != 1 || ((uintptr_t)t.data) % 16) return false;
   const int64_t ps = t.stride[3];
   if (ps % epc || ps < (C + epc - 1) / epc * epc) return false;
@@ -758,7 +780,7 @@ extern "C" int32_t tpg_bn_train_fwd(int32_t n, int32_t c, int32_t h, int32_t w, 
   hipStream_t s = (hipStream_t)stream;
   if (hipError_t e = hipMemsetAsync(ws, 0, sizeof(float) * 2 * c, s)) return (int)e;
   const int blocks = bn_blocks(a);
-  return x.dtype == TPG_BF16 ? bn_launch_fwd<__bf16>(a, blocks, s) : bn_launch_fwd<float>(a, blocks, s);
+  return x.dtype == TPG_F16 ? bn_launch_fwd<_Float16>(a, blocks, s) : x.dtype == TPG_BF16 ? bn_launch_fwd<__bf16>(a, blocks, s) : bn_launch_fwd<float>(a, blocks, s);
 }
 
 extern "C" int32_t tpg_bn_train_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
@@ -780,5 +802,5 @@ extern "C" int32_t tpg_bn_train_bwd(int32_t n, int32_t c, int32_t h, int32_t w, 
   hipStream_t s = (hipStream_t)stream;
   if (hipError_t e = hipMemsetAsync(ws, 0, sizeof(float) * 2 * c, s)) return (int)e;
   const int blocks = bn_blocks(a);
-  return dt == TPG_BF16 ? bn_launch_bwd<__bf16>(a, blocks, s) : bn_launch_bwd<float>(a, blocks, s);
+  return dt == TPG_F16 ? bn_launch_bwd<_Float16>(a, blocks, s) : dt == TPG_BF16 ? bn_launch_bwd<__bf16>(a, blocks, s) : bn_launch_bwd<float>(a, blocks, s);
 }

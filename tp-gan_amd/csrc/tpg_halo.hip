@@ -73,9 +73,10 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
   return a.u;
 }
 
-template <bool BF, int HL, int BN, int WM, int WN, bool MASK>
+template <int DT, int HL, int BN, int WM, int WN, bool MASK>
 __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
-  using E = typename std::conditional<BF, __bf16, float>::type;
+  using E = dt_t<DT>;
+  constexpr bool BF = DT != 0;  // 16-bit operands (bf16 or fp16)
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
   constexpr int KS = 4 * EPC;                // channels per 64-byte step
   constexpr int BM = 256;                    // output rows per block (IMG sub-tiles)
@@ -255,8 +256,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   for (int n = 0; n < NREP - NH; ++n) hb[n] = u32x4{0u, 0u, 0u, 0u};
   auto mma = [&](u32x4 a, u32x4 b, f32x4 c) -> f32x4 {
     if constexpr (BF) {
-      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                     0, 0, 0);
+      return mfma16x16x32<DT>(a, b, c);
     } else {
       const f32x4 a4 = __builtin_bit_cast(f32x4, a);
       const f32x4 b4 = __builtin_bit_cast(f32x4, b);
@@ -560,9 +560,9 @@ size_t halo_lds_bytes(int hcap, int bn, int rs) {
   return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn));
 }
 
-template <bool BF, int HL, int BN, int WM, int WN, bool MASK>
+template <int DT, int HL, int BN, int WM, int WN, bool MASK>
 static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
-  auto k = halo_kernel<BF, HL, BN, WM, WN, MASK>;
+  auto k = halo_kernel<DT, HL, BN, WM, WN, MASK>;
   const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3);
   const int maxl = (int)halo_lds_bytes(HL * 128, BN, 4);
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
@@ -577,13 +577,15 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
   // mask mode: one k-step's y chunks must land (LDS-DMA issued at tap 0) before its halo is
   // staged (last tap): at least two taps, the 3-slot ring, whole 16-pixel DMA rows
   if (mask && (a.ntaps < 2 || (a.var & 2) || a.hcap % 16 || a.SH != 1 || a.SW != 1)) return -1;
-#define X(id, HL_, BN_, WM_, WN_)                                                       \
-  if (cfg == (id)) {                                                                    \
-    if (a.hcap > HL_ * 128) return -1;                                                  \
-    if (mask) return dtype == 1 ? launch_halo_t<true, HL_, BN_, WM_, WN_, true>(a, grid, s)  \
-                                : launch_halo_t<false, HL_, BN_, WM_, WN_, true>(a, grid, s); \
-    return dtype == 1 ? launch_halo_t<true, HL_, BN_, WM_, WN_, false>(a, grid, s)      \
-                      : launch_halo_t<false, HL_, BN_, WM_, WN_, false>(a, grid, s);    \
+#define X(id, HL_, BN_, WM_, WN_)                                                          \
+  if (cfg == (id)) {                                                                       \
+    if (a.hcap > HL_ * 128) return -1;                                                     \
+    if (mask) return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, true>(a, grid, s)    \
+                   : dtype == 2 ? launch_halo_t<2, HL_, BN_, WM_, WN_, true>(a, grid, s)    \
+                                : launch_halo_t<0, HL_, BN_, WM_, WN_, true>(a, grid, s);   \
+    return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, false>(a, grid, s)            \
+         : dtype == 2 ? launch_halo_t<2, HL_, BN_, WM_, WN_, false>(a, grid, s)            \
+                      : launch_halo_t<0, HL_, BN_, WM_, WN_, false>(a, grid, s);           \
   }
   TPG_HALO_CFGS(X)
 #undef X
@@ -609,7 +611,9 @@ size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles) {
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s) {
   const int nchunks = nks * a.ntaps * ntiles * halo_bnl(bn) * 4;
   const int blocks = (nchunks + 255) / 256;
-  if (a.dtype == 1)
+  if (a.dtype == 2)
+    hipLaunchKernelGGL(pack_halo_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles, nchunks);
+  else if (a.dtype == 1)
     hipLaunchKernelGGL(pack_halo_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles, nchunks);
   else
     hipLaunchKernelGGL(pack_halo_kernel<float>, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles, nchunks);

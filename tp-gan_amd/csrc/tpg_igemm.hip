@@ -46,9 +46,10 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-template <bool BF, int BM, int BN, int WM, int WN>
+template <int DT, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
-  using E = typename std::conditional<BF, __bf16, float>::type;
+  using E = dt_t<DT>;
+  constexpr bool BF = DT != 0;
   constexpr int EPC = 16 / sizeof(E);      // elements per 16-byte chunk
   constexpr int CPU = 16 / EPC;            // chunks per 16-channel unit
   constexpr int UPK = 8 / CPU;             // units per 128-byte k-tile
@@ -198,8 +199,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
 #pragma unroll
         for (int n = 0; n < NREP; ++n) {
           if constexpr (BF) {
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[m]),
-                                                                __builtin_bit_cast(bf16x8, bfr[n]), acc[m][n], 0, 0, 0);
+            acc[m][n] = mfma16x16x32<DT>(af[m], bfr[n], acc[m][n]);
           } else {
             f32x4 a4 = __builtin_bit_cast(f32x4, af[m]);
             f32x4 b4 = __builtin_bit_cast(f32x4, bfr[n]);
@@ -328,8 +328,9 @@ int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s) {
   dim3 grid((a.M + bm - 1) / bm, (a.Nout + bn - 1) / bn, a.ksplit);
 #define X(id, BM_, BN_, WM_, WN_)                                                              \
   if (cfg == id) {                                                                             \
-    if (dtype == 1) hipLaunchKernelGGL((igemm_kernel<true, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a); \
-    else hipLaunchKernelGGL((igemm_kernel<false, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);           \
+    if (dtype == 1) hipLaunchKernelGGL((igemm_kernel<1, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);      \
+    else if (dtype == 2) hipLaunchKernelGGL((igemm_kernel<2, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_kernel<0, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);                 \
   }
   TPG_IGEMM_CFGS(X)
 #undef X
@@ -341,7 +342,10 @@ int launch_epilogue(const EpiArgs& a, hipStream_t s) {
   int64_t total = (int64_t)a.M * a.Nout / (v4 ? 4 : 1);
   int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (blocks < 1) blocks = 1;
-  if (a.dtype == 1) {
+  if (a.dtype == 2) {
+    if (v4) hipLaunchKernelGGL((epilogue_kernel<_Float16, 4>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((epilogue_kernel<_Float16, 1>), dim3(blocks), dim3(256), 0, s, a);
+  } else if (a.dtype == 1) {
     if (v4) hipLaunchKernelGGL((epilogue_kernel<__bf16, 4>), dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((epilogue_kernel<__bf16, 1>), dim3(blocks), dim3(256), 0, s, a);
   } else {

@@ -9,6 +9,33 @@
 
 namespace tpg {
 
+// ---------------------------------------------------------------- element types ----
+// Kernel dtype template parameter DT = tpg_conv_desc.dtype: 0 fp32 (parity mode), 1 bf16,
+// 2 fp16.  The two 16-bit types share every layout (8 elements per 16-byte chunk) and differ
+// only in the MFMA opcode and in the bits of 1.0.
+template <int DT> struct DtT { using E = float; };
+template <> struct DtT<1> { using E = __bf16; };
+template <> struct DtT<2> { using E = _Float16; };
+template <int DT> using dt_t = typename DtT<DT>::E;
+
+typedef __attribute__((ext_vector_type(4))) float mf32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 mbf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 mf16x8;
+
+// v_mfma_f32_16x16x32_bf16 / _f16 on two 16-byte fragments given as any 16-byte bit vector
+template <int DT, typename V>
+__device__ __forceinline__ mf32x4 mfma16x16x32(V a, V b, mf32x4 c) {
+  if constexpr (DT == 2)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(mf16x8, a), __builtin_bit_cast(mf16x8, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(mbf16x8, a), __builtin_bit_cast(mbf16x8, b), c,
+                                                   0, 0, 0);
+}
+// two packed 16-bit ones of DT
+template <int DT> __host__ __device__ constexpr uint32_t one_pair() { return DT == 2 ? 0x3C003C00u : 0x3F803F80u; }
+__host__ __device__ constexpr int dt_size(int dtype) { return dtype == 0 ? 4 : 2; }
+
 // Activation codes of tpg_conv_desc.act (include/tpgan.h): 0 none, 1 ReLU,
 // 2 LeakyReLU(slope), 3 ReLU6 (MobileNetV2.py:104,107 / :150,169).
 __device__ __forceinline__ float tpg_act(float v, int act, float slope) {
@@ -129,6 +156,7 @@ typedef WgradArgs Wgrad2Args;
 // Stride-1 Conv2d weight gradient by kernel-row halos (tpg_wgrad_rh.hip): P = dY, Q = X,
 // both dense channels-last; element strides; byte extents < 2^31.
 struct WgradRHArgs {
+  int dtype;                  // 1 bf16, 2 fp16
   const void* P;
   int p_sn, p_sh, p_sw, PH, PW, Ca, p_bytes;
   const void* Q;

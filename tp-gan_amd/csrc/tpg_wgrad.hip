@@ -40,9 +40,10 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   }
 }
 
-template <bool BF, int BM, int BN, int WM, int WN>
+template <int DT, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs p) {
-  using E = typename std::conditional<BF, __bf16, float>::type;
+  using E = dt_t<DT>;
+  constexpr bool BF = DT != 0;
   constexpr int EPC = 16 / sizeof(E);
   constexpr int KP = 32;                  // pixels per k-tile
   constexpr int CPR_A = BM / EPC;         // 16-byte chunks per LDS row
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs p) {
       for (int m = 0; m < MREP; ++m)
 #pragma unroll
         for (int n = 0; n < NREP; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = mfma16x16x32<DT>(af[m], bfr[n], acc[m][n]);
     } else {
       const float* Af = reinterpret_cast<const float*>(As);
       const float* Bf = reinterpret_cast<const float*>(Bs);
@@ -294,8 +295,9 @@ int launch_wgrad(const WgradArgs& a, int dtype, int cfg, hipStream_t s) {
   dim3 grid(((a.Ca + bm - 1) / bm) * ((a.Cb + bn - 1) / bn), a.ntaps, a.ksplit);
 #define X(id, BM_, BN_, WM_, WN_)                                                               \
   if (cfg == id) {                                                                              \
-    if (dtype == 1) hipLaunchKernelGGL((wgrad_kernel<true, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a); \
-    else hipLaunchKernelGGL((wgrad_kernel<false, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);           \
+    if (dtype == 1) hipLaunchKernelGGL((wgrad_kernel<1, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);      \
+    else if (dtype == 2) hipLaunchKernelGGL((wgrad_kernel<2, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((wgrad_kernel<0, BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, a);                 \
   }
   TPG_WGRAD_CFGS(X)
 #undef X

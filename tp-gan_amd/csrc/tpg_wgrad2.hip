@@ -48,9 +48,10 @@ __device__ __forceinline__ int w2_swz(int row) {
   }
 }
 
-template <bool BF, int BM, int BN, int WM, int WN, bool FLAT>
+template <int DT, int BM, int BN, int WM, int WN, bool FLAT>
 __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
-  using E = typename std::conditional<BF, __bf16, float>::type;
+  using E = dt_t<DT>;
+  constexpr bool BF = DT != 0;
   constexpr int ES = sizeof(E);
   constexpr int EPC = 16 / ES;
   constexpr int KP = BF ? 64 : 32;            // pixels per k-tile
@@ -227,9 +228,13 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{one_pair<DT>(), one_pair<DT>(), one_pair<DT>(), one_pair<DT>()});
 
-  auto compute = [&](int slot, bool bias_now) {
+  // BIAS (compile-time): also the bias MFMAs, right beside the regular MFMA that already
+  // holds each A fragment (a runtime branch inside this hand-scheduled region let the compiler
+  // copy the in-flight ds_read_b64_tr_b16 destinations before their wait: stale fragments)
+  auto compute = [&](int slot, auto BIAS) {
+    constexpr bool bias_now = decltype(BIAS)::value;
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     if constexpr (BF) {
@@ -268,19 +273,13 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
           const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * n],
                                                                                h[cur][2 * MREP + 2 * n + 1],
                                                                                0, 1, 2, 3, 4, 5, 6, 7));
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[m][n], 0, 0, 0);
+          acc[m][n] = mfma16x16x32<DT>(av, bv, acc[m][n]);
+          if constexpr (bias_now) {
+            if (n == 0) accb[m] = mfma16x16x32<DT>(av, ones, accb[m]);
+          }
           if (ks + 1 < NS) {
 #pragma unroll
             for (int r = i * R / M; r < (i + 1) * R / M; ++r) h[cur ^ 1][r] = tr_read(addr(ks + 1, r));
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (bias_now) {
-#pragma unroll
-          for (int m = 0; m < MREP; ++m) {
-            const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
-                                                                                 0, 1, 2, 3, 4, 5, 6, 7));
-            accb[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, ones, accb[m], 0, 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -309,7 +308,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 #pragma unroll
           for (int n = 0; n < NREP; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
-        if (bias_now) {
+        if constexpr (bias_now) {
 #pragma unroll
           for (int m = 0; m < MREP; ++m) accb[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], 1.0f, accb[m], 0, 0, 0);
         }
@@ -334,7 +333,8 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
     for (int kt = 0; kt < nkt; ++kt) {
       const int slot2 = slot == 0 ? 2 : slot - 1;
       issue(min(kt + 2, nkt - 1), slot2);  // unconditional (clamped): static vmcnt
-      compute(slot, bias_wave && (kt_base + kt) % p.bshare == sid);
+      if (bias_wave && (kt_base + kt) % p.bshare == sid) compute(slot, std::true_type{});
+      else compute(slot, std::false_type{});
       W2_WAIT_BARRIER();                   // retires k-tile kt+1, kt+2 stays in flight
       slot = slot == 2 ? 0 : slot + 1;
     }
@@ -407,15 +407,17 @@ static int launch_wgrad2_t(const Wgrad2Args& a, int dtype, int cfg, int bm, int 
   dim3 grid(((a.Ca + bm - 1) / bm) * ((ncols + bn - 1) / bn) * (FLAT ? 1 : a.ntaps) * a.ksplit);
 #define X(id, BM_, BN_, WM_, WN_)                                                                       \
   if (cfg == (id)) {                                                                                    \
-    if (dtype == 1) {                                                                                   \
-      auto k = wgrad2_kernel<true, BM_, BN_, WM_, WN_, FLAT>;                                           \
+    if (dtype != 0) {                                                                                   \
+      auto k = dtype == 2 ? wgrad2_kernel<2, BM_, BN_, WM_, WN_, FLAT> : wgrad2_kernel<1, BM_, BN_, WM_, WN_, FLAT>; \
       const size_t lds = 3 * 64 * (BM_ + BN_) * 2;                                                      \
-      static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                                    (int)lds), true);                                   \
-      (void)once;                                                                                       \
+      static bool once1 = ((void)hipFuncSetAttribute((const void*)wgrad2_kernel<1, BM_, BN_, WM_, WN_, FLAT>, \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true); \
+      static bool once2 = ((void)hipFuncSetAttribute((const void*)wgrad2_kernel<2, BM_, BN_, WM_, WN_, FLAT>, \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true); \
+      (void)once1; (void)once2;                                                                         \
       hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                \
     } else {                                                                                            \
-      auto k = wgrad2_kernel<false, BM_, BN_, WM_, WN_, FLAT>;                                          \
+      auto k = wgrad2_kernel<0, BM_, BN_, WM_, WN_, FLAT>;                                              \
       const size_t lds = 3 * 32 * (BM_ + BN_) * 4;                                                      \
       static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                                     (int)lds), true);                                   \

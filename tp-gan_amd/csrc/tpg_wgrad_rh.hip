@@ -16,6 +16,7 @@
 // pixel splits.  Blocks of one pixel split are adjacent in the XCD-aware order, so the
 // tiles that read the same dY / X rows run together on one XCD's L2.
 #include "tpg_internal.h"
+#include <type_traits>
 
 namespace tpg {
 
@@ -45,7 +46,7 @@ __device__ __forceinline__ int rh_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-template <int NR, int NT, int BM, int BC>
+template <int DT, int NR, int NT, int BM, int BC>
 __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   // k-tile: 64 pixels = TH x TW (TW = p.tw: a row segment of 64, or TH = 64 / TW whole rows of
   // a narrower map); block taps: NR kernel rows x NT columns (row mode NR = 1, image mode
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
 #pragma unroll
     for (int j = 0; j < NREP; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});  // 1.0 bf16
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{one_pair<DT>(), one_pair<DT>(), one_pair<DT>(), one_pair<DT>()});
 
   // Fragment reads (transposed, 4 channels x 4 pixels per lane and read): fragment r < 2*MREP
   // is dY (A), the rest X halo rows shifted by the column's tap.  Next substep's reads are
@@ -178,7 +179,10 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       const int k = ks * 32 + 8 * g + 4 * h + q;
       kbase[ks][h] = (k / TW) * HW + k % TW;
     }
-  auto compute = [&](int slot, bool bias_now) {
+  // BIAS (compile-time): the bias MFMAs sit beside the regular MFMA holding each A fragment
+  // (see tpg_wgrad2.hip: no runtime branch inside this hand-scheduled region)
+  auto compute = [&](int slot, auto BIAS) {
+    constexpr bool bias_now = decltype(BIAS)::value;
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     constexpr int NS = KP / 32;
@@ -211,19 +215,13 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * j],
                                                                              h[cur][2 * MREP + 2 * j + 1],
                                                                              0, 1, 2, 3, 4, 5, 6, 7));
-        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[m][j], 0, 0, 0);
+        acc[m][j] = mfma16x16x32<DT>(av, bv, acc[m][j]);
+        if constexpr (bias_now) {
+          if (j == 0) accb[m] = mfma16x16x32<DT>(av, ones, accb[m]);
+        }
         if (ks + 1 < NS) {
 #pragma unroll
           for (int rr = i * R / M; rr < (i + 1) * R / M; ++rr) h[cur ^ 1][rr] = rh_tr_read(addr(ks + 1, rr));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (bias_now) {  // dbias: the substep's A fragments against ones (h[cur] is not overwritten yet)
-#pragma unroll
-        for (int m = 0; m < MREP; ++m) {
-          const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
-                                                                               0, 1, 2, 3, 4, 5, 6, 7));
-          accb[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, ones, accb[m], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -256,7 +254,8 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   int slot = 0;
   for (int kt = 0; kt < nkt; ++kt) {
     issue_next(slot == 0 ? 2 : slot - 1);
-    compute(slot, bias_wave && (kt0 + kt) % p.bshare == sid);
+    if (bias_wave && (kt0 + kt) % p.bshare == sid) compute(slot, std::true_type{});
+    else compute(slot, std::false_type{});
     RH_WAIT_BARRIER();  // retires k-tile kt+1, kt+2 stays in flight
     slot = slot == 2 ? 0 : slot + 1;
   }
@@ -314,11 +313,13 @@ template <int NR, int NT, int BM, int BC>
 static int launch_rh_t(const WgradRHArgs& a, hipStream_t s) {
   constexpr int GB = (((NR == 1 ? 72 : 200) * BC * 2 + 1023) / 1024 + 7) / 8;
   const size_t lds = 3 * (64 * BM * 2 + GB * 8 * 1024);
-  auto k = wgrad_rh_kernel<NR, NT, BM, BC>;
-  static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+  auto k1 = wgrad_rh_kernel<1, NR, NT, BM, BC>;
+  auto k2 = wgrad_rh_kernel<2, NR, NT, BM, BC>;
+  static bool once = ((void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                      (void)hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                       true);
   (void)once;
-  hipLaunchKernelGGL(k, dim3(a.tiles * a.ksplit), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(a.dtype == 2 ? k2 : k1, dim3(a.tiles * a.ksplit), dim3(512), lds, s, a);
   return (int)hipGetLastError();
 }
 

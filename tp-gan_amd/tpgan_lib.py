@@ -15,7 +15,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtpgan_hip.so")
 
-TPG_F32, TPG_BF16 = 0, 1
+TPG_F32, TPG_BF16, TPG_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3
 PAD_ZERO, PAD_REFLECT = 0, 1
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
@@ -135,11 +135,13 @@ def dtype_code(dt):
         return TPG_F32
     if dt == torch.bfloat16:
         return TPG_BF16
-    raise TypeError("tpgan ops support float32 and bfloat16, got %s" % dt)
+    if dt == torch.float16:
+        return TPG_F16
+    raise TypeError("tpgan ops support float32, bfloat16 and float16, got %s" % dt)
 
 
 def dtype_from_code(code):
-    return torch.bfloat16 if code == TPG_BF16 else torch.float32
+    return {TPG_BF16: torch.bfloat16, TPG_F16: torch.float16}.get(code, torch.float32)
 
 
 def tt(t):

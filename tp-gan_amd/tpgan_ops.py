@@ -7,7 +7,8 @@ with channel stride 1; anything else (e.g. the user's NCHW fp32 images) is conve
 the device by tpg_copy4d.
 
 Compute dtype: float32 by default (the reference's precision; MFMA f32 path), or
-bfloat16 inside `with compute_dtype(torch.bfloat16):` (MFMA bf16 path, fp32 accumulate).
+bfloat16 / float16 inside `with compute_dtype(torch.bfloat16)` (or torch.float16): the 16-bit MFMA
+paths, fp32 accumulate.
 Master weights and their gradients stay float32.
 """
 import contextlib
@@ -18,7 +19,8 @@ import torch
 
 from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
                        PAD_REFLECT,
-                       PAD_ZERO, TPG_BF16, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load, stream_ptr, tt)
+                       PAD_ZERO, TPG_BF16, TPG_F32, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load,
+                       stream_ptr, tt)
 
 _DTYPE = [torch.float32]
 
@@ -241,7 +243,7 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     hit = AUTOTUNE["cache"].get(key)
     if hit is not None:
         return hit
-    if not AUTOTUNE["enabled"] or d.dtype != TPG_BF16:
+    if not AUTOTUNE["enabled"] or d.dtype == TPG_F32:
         return (0, 0)
     scratch = torch.empty_strided(dwv.shape, dwv.stride(), dtype=torch.float32, device=dwv.device)
     npix = d.n * (d.in_h * d.in_w if d.transposed else d.out_h * d.out_w)
@@ -321,7 +323,7 @@ def _packed_weight(param, d, op, w):
     """The packed image of w for (d, op) if param is FlatParams-managed, packing it now if
     it was not packed since the last update; None otherwise."""
     flat = getattr(param, "_tpg_flat", None)
-    if flat is None or not PACK["enabled"] or d.dtype != TPG_BF16 or w.dtype != torch.float32:
+    if flat is None or not PACK["enabled"] or d.dtype == TPG_F32 or w.dtype != torch.float32:
         return None
     key = (op, _desc_tuple(d), w.data_ptr(), tuple(w.stride()))
     e = _pack_entry(flat, key, d, op, w)
@@ -352,10 +354,10 @@ def repack(flat):
         e.epoch = flat.epoch
 
 
-def _packed_tt(buf):
+def _packed_tt(buf, dtype=TPG_BF16):
     t = TpgTensor()
     t.data = buf.data_ptr()
-    t.dtype = TPG_BF16
+    t.dtype = dtype  # (a packed image is flagged by the descriptor; the field is informational)
     return t
 
 
@@ -513,7 +515,7 @@ def _conv_act_backward_fused(ctx, gy):
     need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
     need_db = ctx.has_bias and ctx.needs_input_grad[2]
     gy = _fix_c1(gy)
-    es = 2 if dtype == torch.bfloat16 else 4
+    es = 4 if dtype == torch.float32 else 2
     g_is_gy = (ctx.act == ACT_NONE and gy.dtype == dtype and gy.dim() == 4 and gy.stride(1) == 1 and
                gy.data_ptr() % 16 == 0 and all((gy.stride(i) * es) % 16 == 0 for i in (0, 2, 3)))
     g = gy if g_is_gy else _fix_c1(new_act(n, cout, oh, ow, dtype, y.device))
@@ -539,7 +541,7 @@ def _conv_act_backward_fused(ctx, gy):
     # the weight-gradient tile / split is autotuned on a shape's first call, which needs g:
     # that call runs the fused op without dW, tunes on its g, then runs the weight gradient
     key = _wgrad_key(d)
-    tune_first = (need_dw and AUTOTUNE["enabled"] and d.dtype == TPG_BF16 and key not in AUTOTUNE["cache"])
+    tune_first = (need_dw and AUTOTUNE["enabled"] and d.dtype != TPG_F32 and key not in AUTOTUNE["cache"])
     if need_dw and not tune_first:
         d.algo, d.ksplit = AUTOTUNE["cache"].get(key, (0, 0))
     if need_dx:
@@ -824,7 +826,7 @@ class _LocalFuse(torch.autograd.Function):
         tts = []
         for i, (shp, dt) in enumerate(zip(ctx.shapes, ctx.dtypes)):
             if ctx.needs_input_grad[1 + i]:
-                gdt = dt if dt in (torch.float32, torch.bfloat16) else torch.float32
+                gdt = dt if dt in (torch.float32, torch.bfloat16, torch.float16) else torch.float32
                 gi = new_act(*shp, dtype=gdt, device=gy.device)
                 grads.append(gi)
                 tts.append(tt(_fix_c1(gi)))

@@ -327,8 +327,16 @@ class TPGANTrainer:
 
     def __init__(self, G, D, lr=1e-4, betas=(0.5, 0.999), compute_dtype=torch.bfloat16, loss_weights=None,
                  gradient_penalty=False, process_group=None, identity_fn=None, use_dropout=True, overlap=True,
-                 bucket_mb=32.0):
+                 bucket_mb=32.0, loss_scale=None):
         self.G, self.D = G, D
+        # fp16 activations / gradients (BASELINE configs[4]): a static loss scale keeps the
+        # per-element image gradients (~1/(B*3*H*W)) out of fp16's subnormal range; the scale
+        # is divided out in the Adam launch (grad_scale), weight gradients accumulate in fp32
+        if loss_scale is None:
+            loss_scale = 1024.0 if compute_dtype == torch.float16 else 1.0
+        if gradient_penalty and loss_scale != 1.0:
+            raise ValueError("WGAN-GP with a loss scale is not supported (fp16: use bf16 for the GP run)")
+        self.loss_scale = float(loss_scale)
         self.use_dropout = use_dropout  # FeaturePredict dropout (D_and_G_model.py:331-348)
         dev = next(G.parameters()).device
         self.fG = FlatParams(G, dev)
@@ -373,7 +381,7 @@ class TPGANTrainer:
             loss_D = d_fake.mean() - d_real.mean()
             if self.gp:
                 loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
-            loss_D.backward()
+            (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
 
     def gradient_penalty(self, real, fake, alpha=None):
@@ -395,7 +403,7 @@ class TPGANTrainer:
         D = self.D
         fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = self._st.pop("outs")
         with tpgan_ops.compute_dtype(self.dtype):
-            self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
+            self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale)
             # ---- G-step through the frozen, updated D
             set_requires_grad(D.parameters(), False)
             d_gen = D(fake).float()
@@ -418,11 +426,11 @@ class TPGANTrainer:
             loss_G = loss_G + w["weight_identity_preserving"] * self.identity_fn(f32, front)
         if self.gsync is not None and not self._capturing:
             self.gsync.begin()
-        loss_G.backward()
+        (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
         self._st["loss_G"] = loss_G.detach()
 
     def _phase_c(self, b):
-        self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale)
+        self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale)
         return {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
 
     # ---- checkpoint / resume.  Files and formats of the reference's
@@ -551,16 +559,19 @@ class TPGANTrainer:
         return self._graph_out
 
 
-def synthetic_batch(B, device, seed=0):
-    """Multi-PIE-shaped synthetic batch, U[-1, 1] images (DataAndDataset.py:220), z, labels."""
+def synthetic_batch(B, device, seed=0, img_size=128):
+    """Multi-PIE-shaped synthetic batch, U[-1, 1] images (DataAndDataset.py:220), z, labels.
+    img_size 256 (BASELINE configs[4]) doubles the face and the patch sizes (LocalFuser(256))."""
     g = torch.Generator(device="cpu").manual_seed(seed)
+    k = img_size // 128
 
     def u(*s):
         return (torch.rand(*s, generator=g) * 2 - 1).to(device)
 
-    b = {"I128": u(B, 3, 128, 128), "left_eye": u(B, 3, 40, 40), "right_eye": u(B, 3, 40, 40),
-         "nose": u(B, 3, 32, 40), "mouth": u(B, 3, 32, 48), "z": u(B, 64), "frontal": u(B, 3, 128, 128),
-         "frontal_left_eye": u(B, 3, 40, 40), "frontal_right_eye": u(B, 3, 40, 40), "frontal_nose": u(B, 3, 32, 40),
-         "frontal_mouth": u(B, 3, 32, 48),
+    S, E, NH, NW, MH, MW = img_size, 40 * k, 32 * k, 40 * k, 32 * k, 48 * k
+    b = {"I128": u(B, 3, S, S), "left_eye": u(B, 3, E, E), "right_eye": u(B, 3, E, E),
+         "nose": u(B, 3, NH, NW), "mouth": u(B, 3, MH, MW), "z": u(B, 64), "frontal": u(B, 3, S, S),
+         "frontal_left_eye": u(B, 3, E, E), "frontal_right_eye": u(B, 3, E, E), "frontal_nose": u(B, 3, NH, NW),
+         "frontal_mouth": u(B, 3, MH, MW),
          "label": torch.randint(0, 347, (B,), generator=g).to(device)}
     return b
