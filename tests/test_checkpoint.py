@@ -52,10 +52,12 @@ def test_optimizer_state_shape_mismatch_raises():
 @pytest.mark.gpu
 def test_trainer_resume_matches_uninterrupted(gpu, tmp_path):
     """Train 2 steps, checkpoint, train 1 more; a fresh trainer (other weights) that loads the
-    checkpoint and trains the same step lands on the same weights and moments."""
+    checkpoint and trains the same step lands on the same weights and moments (deterministic
+    mode: bit-identical)."""
     import D_and_G_model as DG
+    import tpgan_ops
     import tpgan_train
-    from _cases import load_det, rel
+    from _cases import load_det
 
     def models(seed):
         torch.manual_seed(seed)
@@ -65,6 +67,12 @@ def test_trainer_resume_matches_uninterrupted(gpu, tmp_path):
             load_det(D, "D/", torch.float32)
         return G.to(gpu), D.to(gpu)
 
+    with tpgan_ops.deterministic():
+        _resume_case(gpu, tmp_path, models)
+
+
+def _resume_case(gpu, tmp_path, models):
+    import tpgan_train
     b = tpgan_train.synthetic_batch(2, gpu, seed=4)
     G, D = models(0)
     tr = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.float32, use_dropout=False)
@@ -84,9 +92,9 @@ def test_trainer_resume_matches_uninterrupted(gpu, tmp_path):
     torch.cuda.synchronize()
     for f1, f2 in ((tr.fG, tr2.fG), (tr.fD, tr2.fD)):
         assert float(f2.adam_state[0]) == 3.0
-        # same step on the same state; only the fp32 atomics order of the weight gradients differs
-        assert rel(f2.data.cpu(), f1.data.cpu()) < 1e-5
-        assert rel(f2.exp_avg.cpu(), f1.exp_avg.cpu()) < 1e-3
+        # same step on the same state, no split-K atomics: the same bits
+        assert torch.equal(f2.data, f1.data)
+        assert torch.equal(f2.exp_avg, f1.exp_avg) and torch.equal(f2.exp_avg_sq, f1.exp_avg_sq)
 
 
 class _Tiny(torch.nn.Module):

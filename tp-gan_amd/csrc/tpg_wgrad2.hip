@@ -233,8 +233,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
   // BIAS (compile-time): also the bias MFMAs, right beside the regular MFMA that already
   // holds each A fragment (a runtime branch inside this hand-scheduled region let the compiler
   // copy the in-flight ds_read_b64_tr_b16 destinations before their wait: stale fragments)
-  auto compute = [&](int slot, auto BIAS) {
-    constexpr bool bias_now = decltype(BIAS)::value;
+  auto compute = [&](int slot, bool bias_now) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     if constexpr (BF) {
@@ -274,9 +273,6 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
                                                                                h[cur][2 * MREP + 2 * n + 1],
                                                                                0, 1, 2, 3, 4, 5, 6, 7));
           acc[m][n] = mfma16x16x32<DT>(av, bv, acc[m][n]);
-          if constexpr (bias_now) {
-            if (n == 0) accb[m] = mfma16x16x32<DT>(av, ones, accb[m]);
-          }
           if (ks + 1 < NS) {
 #pragma unroll
             for (int r = i * R / M; r < (i + 1) * R / M; ++r) h[cur ^ 1][r] = tr_read(addr(ks + 1, r));
@@ -287,6 +283,20 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
         }
+      }
+      // bias (dY row sums) of an owned k-tile, after the hand-scheduled region: the A fragments
+      // of both substeps are still in h (substep 1 read into h[1]) and every read has been
+      // waited on.  (Bias MFMAs inside the region needed a second, compile-time copy of it,
+      // which doubled its hoisted LDS addresses and spilled the wide tiles.)
+      static_assert(NS == 2, "h holds both substeps");
+      if (bias_now) {
+      #pragma unroll
+        for (int ks = 0; ks < NS; ++ks)
+      #pragma unroll
+          for (int m = 0; m < MREP; ++m)
+            accb[m] = mfma16x16x32<DT>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(h[ks][2 * m], h[ks][2 * m + 1],
+                                                                                         0, 1, 2, 3, 4, 5, 6, 7)),
+                                       ones, accb[m]);
       }
     } else {
 #pragma unroll
@@ -308,7 +318,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
 #pragma unroll
           for (int n = 0; n < NREP; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
-        if constexpr (bias_now) {
+        if (bias_now) {
 #pragma unroll
           for (int m = 0; m < MREP; ++m) accb[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], 1.0f, accb[m], 0, 0, 0);
         }
@@ -333,8 +343,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
     for (int kt = 0; kt < nkt; ++kt) {
       const int slot2 = slot == 0 ? 2 : slot - 1;
       issue(min(kt + 2, nkt - 1), slot2);  // unconditional (clamped): static vmcnt
-      if (bias_wave && (kt_base + kt) % p.bshare == sid) compute(slot, std::true_type{});
-      else compute(slot, std::false_type{});
+      compute(slot, bias_wave && (kt_base + kt) % p.bshare == sid);  // (one inlined copy)
       W2_WAIT_BARRIER();                   // retires k-tile kt+1, kt+2 stays in flight
       slot = slot == 2 ? 0 : slot + 1;
     }

@@ -181,8 +181,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
     }
   // BIAS (compile-time): the bias MFMAs sit beside the regular MFMA holding each A fragment
   // (see tpg_wgrad2.hip: no runtime branch inside this hand-scheduled region)
-  auto compute = [&](int slot, auto BIAS) {
-    constexpr bool bias_now = decltype(BIAS)::value;
+  auto compute = [&](int slot, bool bias_now) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     constexpr int NS = KP / 32;
@@ -216,9 +215,6 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
                                                                              h[cur][2 * MREP + 2 * j + 1],
                                                                              0, 1, 2, 3, 4, 5, 6, 7));
         acc[m][j] = mfma16x16x32<DT>(av, bv, acc[m][j]);
-        if constexpr (bias_now) {
-          if (j == 0) accb[m] = mfma16x16x32<DT>(av, ones, accb[m]);
-        }
         if (ks + 1 < NS) {
 #pragma unroll
           for (int rr = i * R / M; rr < (i + 1) * R / M; ++rr) h[cur ^ 1][rr] = rh_tr_read(addr(ks + 1, rr));
@@ -229,6 +225,20 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
+    // bias (dY row sums) of an owned k-tile, after the hand-scheduled region: the A fragments
+    // of both substeps are still in h (substep 1 read into h[1]) and every read has been
+    // waited on.  (Bias MFMAs inside the region needed a second, compile-time copy of it,
+    // which doubled its hoisted LDS addresses and spilled the wide tiles.)
+    static_assert(NS == 2, "h holds both substeps");
+    if (bias_now) {
+    #pragma unroll
+      for (int ks = 0; ks < NS; ++ks)
+    #pragma unroll
+        for (int m = 0; m < MREP; ++m)
+          accb[m] = mfma16x16x32<DT>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(h[ks][2 * m], h[ks][2 * m + 1],
+                                                                                       0, 1, 2, 3, 4, 5, 6, 7)),
+                                     ones, accb[m]);
     }
   };
 
@@ -254,8 +264,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   int slot = 0;
   for (int kt = 0; kt < nkt; ++kt) {
     issue_next(slot == 0 ? 2 : slot - 1);
-    if (bias_wave && (kt0 + kt) % p.bshare == sid) compute(slot, std::true_type{});
-    else compute(slot, std::false_type{});
+    compute(slot, bias_wave && (kt0 + kt) % p.bshare == sid);  // (one inlined copy)
     RH_WAIT_BARRIER();  // retires k-tile kt+1, kt+2 stays in flight
     slot = slot == 2 ? 0 : slot + 1;
   }
