@@ -90,7 +90,9 @@ typedef struct tpg_conv_desc {
                                      64x32 (stride-1 bf16 Conv2d, 3/5/7-wide kernels, output
                                      width a multiple of 64); 10, 11 = image-halo kernel, tile
                                      128x32, 64x32 (2x2 / 3x3 kernels, output width 8/16/32/64·m,
-                                     64 / width dividing the height); -30 when not covered */
+                                     64 / width dividing the height); 12 = kernel-row halo kernel,
+                                     tile 256x32 (one a-tile up to 256 output channels: dY read
+                                     once per b-tile); -30 when not covered */
   int32_t flags;                  /* TPG_FLAG_*: WPACKED = w.data is the image tpg_conv2d_pack_jobs /
                                      tpg_pack_run produced for this descriptor and op */
 } tpg_conv_desc;

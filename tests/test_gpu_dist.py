@@ -1,5 +1,5 @@
 """GPU, world_size 2 on ONE device (two processes sharing cuda:0, gloo over CUDA tensors):
-the data-parallel train step with the bucketed, backward-overlapped G all-reduce
+the data-parallel train step with the bucketed, backward-overlapped G and D all-reduces
 (tpgan_train.OverlappedGradSync) keeps the replicas bit-identical, issues buckets during
 the backward, and learns the same bucket layout on both ranks.  (RCCL needs one device
 per rank; the 8-GPU RCCL run is the driver's scaling bench.)"""
@@ -38,23 +38,27 @@ def _worker(rank, world, port, q):
         D = DG.Discriminator().to(dev)
         tr = tpgan_train.TPGANTrainer(G, D, compute_dtype=torch.bfloat16, bucket_mb=16.0)
         b = tpgan_train.synthetic_batch(2, dev, seed=100 + rank)
-        issued_early = []
-        orig_finish = tr.gsync.finish
+        issued_early, d_early = [], []
 
-        def finish():
-            issued_early.append(tr.gsync.next)  # buckets already issued when backward returned
-            return orig_finish()
+        def wrap(sync, out):
+            orig = sync.finish
 
-        tr.gsync.finish = finish
+            def finish():
+                out.append(sync.next)  # buckets already issued when the backward returned
+                return orig()
+            sync.finish = finish
+
+        wrap(tr.gsync, issued_early)
+        wrap(tr.dsync, d_early)
         for _ in range(3):
             tr.step(b)
         torch.cuda.synchronize()
         sums = torch.stack([tr.fG.data.double().sum(), tr.fD.data.double().sum(),
                             tr.fG.data.double().square().sum()]).cpu()
         q.put((rank, sums.tolist(), issued_early, len(tr.gsync.buckets), list(tr.fG.offsets[:50]),
-               tr.gsync.order_learned))
+               tr.gsync.order_learned, d_early, len(tr.dsync.buckets), tr.dsync.order_learned))
     except Exception as e:
-        q.put((rank, repr(e), [], 0, [], False))
+        q.put((rank, repr(e), [], 0, [], False, [], 0, False))
         raise
     finally:
         dist.destroy_process_group()
@@ -72,12 +76,15 @@ def test_dp_overlap_two_ranks_one_gpu(gpu):
     res = sorted([q.get(timeout=280) for _ in range(world)])
     for p in procs:
         p.join(60)
-    (r0, s0, e0, nb0, off0, l0), (r1, s1, e1, nb1, off1, l1) = res
+    (r0, s0, e0, nb0, off0, l0, de0, dnb0, dl0), (r1, s1, e1, nb1, off1, l1, de1, dnb1, dl1) = res
     assert isinstance(s0, list) and isinstance(s1, list), (s0, s1)
     assert s0 == s1  # identical replicas after 3 steps
     assert nb0 == nb1 and nb0 > 10 and l0 and l1
     assert off0 == off1
     assert max(e0) > 0 and max(e1) > 0  # some buckets went out while the backward was running
+    # D: bucketed during the D-step backward as well
+    assert dnb0 == dnb1 and dnb0 > 3 and dl0 and dl1
+    assert max(de0) > 0 and max(de1) > 0
 
 
 LR_EQ = 1e-4  # the bench's learning rate

@@ -51,7 +51,7 @@ def flops(s):
     return 2 * N * OH * OW * Cout * Cin * k * k
 
 
-def run(name, s, iters, passes):
+def run(name, s, iters, passes, sweep=False):
     lib = load()
     dev = torch.device("cuda", 0)
     N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
@@ -80,6 +80,27 @@ def run(name, s, iters, passes):
                                                          stream_ptr())),
     }
     f = flops(s)
+    if sweep:  # every weight-gradient (algo, pixel split) the tuner would try
+        res = []
+        for algo in range(1, 13):
+            for ks in (1, 2, 4, 8, 16, 32, 64):
+                d.algo, d.ksplit = algo, ks
+                rc = lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0, stream_ptr())
+                if rc:
+                    break
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(iters):
+                    lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0, stream_ptr())
+                e1.record()
+                torch.cuda.synchronize()
+                res.append((e0.elapsed_time(e1) / iters, algo, ks))
+        d.algo, d.ksplit = 0, 0
+        res.sort()
+        print("%-12s wgrad sweep best: %s" % (name, "  ".join("a%d/k%d %.3f ms %.0f TF/s" % (a_, k_, ms, f / ms / 1e9)
+                                                          for ms, a_, k_ in res[:6])), flush=True)
+        return
     out = []
     for kind, fn in calls.items():
         if kind not in passes:
@@ -104,11 +125,12 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--wg-sweep", action="store_true", help="time every weight-gradient algo / pixel split")
     a = ap.parse_args()
     for name, s in SHAPES.items():
         if a.only and name not in a.only.split(","):
             continue
-        run(name, s, a.iters, a.passes.split(","))
+        run(name, s, a.iters, a.passes.split(","), a.wg_sweep)
 
 
 if __name__ == "__main__":

@@ -779,7 +779,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   a.tw = img ? tw : 64;
   // tile: fewest padded MACs, the 128 x 64 tile (best operand reuse) on ties
   int bm = 128, bc = 64;
-  if (d->algo >= 6 && d->algo <= 11) {
+  if (d->algo >= 6 && d->algo <= 12) {
     a.cfg = d->algo - 6;
     wgrad_rh_tile(a.cfg, &bm, &bc);
   } else {
@@ -800,7 +800,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   } else {
     // pixel splits: whole rounds of resident blocks (one per CU, two for the <= 128-VGPR
     // tiles) against the fp32 atomics every extra split adds (~1.3 TB/s of added bytes)
-    const int resident = (img ? 256 : (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256) / g_share;
+    const int resident = (img || a.cfg == 6 ? 256 : (a.cfg == 3 || (a.cfg != 0 && a.nt <= 4)) ? 512 : 256) / g_share;
     const int taps = a.nr * a.nt;
     const double flops = 2.0 * a.tiles * bm * taps * bc * 64.0 * a.nkt;
     double best = -1;
@@ -876,7 +876,7 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
   // kernel-row halo kernel (stride-1 Conv2d, bf16, 64-pixel row segments): algo 6, and the
   // default for untuned calls when it applies
   static const bool rh_on = !getenv("TPG_WGRAD_RH") || atoi(getenv("TPG_WGRAD_RH")) != 0;  // A/B hook
-  const bool rh_algo = d->algo >= 6 && d->algo <= 11;
+  const bool rh_algo = d->algo >= 6 && d->algo <= 12;
   if (((d->algo == 0 && rh_on) || rh_algo) && !comp && !d->transposed) {
     const int rc = wgrad_rh(d, x, g, dw, dbias, (hipStream_t)stream);
     if (rc != 1) {

@@ -255,9 +255,11 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   do {                                                                                             \
     if constexpr (GA + GB == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
     else if constexpr (GA + GB == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
-    else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
+    else if constexpr (GA + GB == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else if constexpr (GA + GB == 5) asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
   } while (0)
-  static_assert(GA + GB >= 2 && GA + GB <= 4, "vmcnt");
+  static_assert(GA + GB >= 2 && GA + GB <= 6, "vmcnt");
   issue_next(0);
   issue_next(1);
   RH_WAIT_BARRIER();  // retires k-tile 0
@@ -302,14 +304,16 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   }
 }
 
-// tile configs {id, BM, BC}; id = desc.algo - 6 (ids 4, 5: image mode, 32-channel b tiles)
+// tile configs {id, BM, BC}; id = desc.algo - 6 (ids 4, 5: image mode, 32-channel b tiles;
+// id 6: row mode, 256 dY channels per block, waves 64 x (NT x 32) / 2)
 #define TPG_WGRAD_RH_CFGS(X) \
   X(0, 128, 64)              \
   X(1, 128, 32)              \
   X(2, 64, 64)               \
   X(3, 64, 32)               \
   X(4, 128, 32)              \
-  X(5, 64, 32)
+  X(5, 64, 32)               \
+  X(6, 256, 32)
 
 int wgrad_rh_tile(int cfg, int* bm, int* bc) {
 #define X(id, BM_, BC_) if (cfg == (id)) { *bm = BM_; *bc = BC_; return 0; }
@@ -335,7 +339,7 @@ static int launch_rh_t(const WgradRHArgs& a, hipStream_t s) {
 // row-mode configs instantiate the 1 x {3,4,5} tap groups, image-mode ones the 2x2 / 3x3
 template <int ID, int BM, int BC>
 static int launch_rh_cfg(const WgradRHArgs& a, hipStream_t s) {
-  if constexpr (ID < 4) {
+  if constexpr (ID < 4 || ID == 6) {
     if (a.nr == 1 && a.nt == 3) return launch_rh_t<1, 3, BM, BC>(a, s);
     if (a.nr == 1 && a.nt == 4) return launch_rh_t<1, 4, BM, BC>(a, s);
     if (a.nr == 1 && a.nt == 5) return launch_rh_t<1, 5, BM, BC>(a, s);

@@ -14,6 +14,8 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtpgan_hip.so")
+if os.environ.get("TPG_LIB_PATH"):  # A/B builds of the same library (tools/ only)
+    LIB_PATH = os.environ["TPG_LIB_PATH"]
 
 TPG_F32, TPG_BF16, TPG_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3

@@ -250,7 +250,7 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     nkt = (npix + 63) // 64
     best, best_ms = (0, 0), None
     torch.cuda.synchronize()
-    for algo in range(1, 12):
+    for algo in range(1, 13):
         for ks in _WG_SPLITS:
             if ks > nkt or (ks > 16 and (d.flags & FLAG_CONCURRENT)):
                 break
@@ -262,7 +262,7 @@ def _tuned_wgrad(lib, d, x, g, dwv):
                 e0.record()
                 rc = lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(scratch), None, 0, stream_ptr())
                 e1.record()
-                if rc == -30:  # algos 6..11 (row / image-halo kernel) do not cover this shape
+                if rc == -30:  # algos 6..12 (row / image-halo kernel) do not cover this shape
                     break
                 check(rc)
                 e1.synchronize()

@@ -347,22 +347,30 @@ class TPGANTrainer:
         self.gp = gradient_penalty
         self.sync = GradSync(process_group)
         self.world = self.sync.world
-        # G's 551 MB of gradients are reduced bucket by bucket during the G backward
+        # G's 551 MB of gradients are reduced bucket by bucket during the G backward, D's 54 MB
+        # during the D-step backward (buckets of bucket_mb / 4: D's backward is ~5x shorter)
         self.gsync = OverlappedGradSync(self.fG, process_group, bucket_mb) if (overlap and self.world > 1) else None
+        # (not with WGAN-GP: D's parameters then get a second gradient contribution from the
+        # double backward after their first one has been reported ready)
+        self.dsync = (OverlappedGradSync(self.fD, process_group, bucket_mb / 4.0)
+                      if (overlap and self.world > 1 and not gradient_penalty) else None)
         self._capturing = False
         self.identity_fn = identity_fn
         self.sync.broadcast(self.fG)
         self.sync.broadcast(self.fD)
 
     def _allreduce(self, flat):
-        if flat is self.fG and self.gsync is not None and self.gsync.active:
-            self.gsync.finish()
+        ov = self.gsync if flat is self.fG else self.dsync
+        if ov is not None and ov.active:
+            ov.finish()
         else:
             self.sync.allreduce(flat)
 
     # The step is three device phases separated by the two data-parallel exchanges:
     #   A: zero grads, G forward, D-step forward/backward           -> all-reduce D grads
     #   B: D Adam, G-step D forward, G losses, G backward            -> all-reduce G grads
+    # (world > 1, eager: each exchange is bucketed and overlapped with its backward; the
+    # phase boundary only waits for the last buckets)
     #   C: G Adam
     # Eager mode runs them back to back; graph mode (capture()) records each phase as a
     # hipGraph sharing one memory pool and replays them around the RCCL calls.
@@ -381,6 +389,8 @@ class TPGANTrainer:
             loss_D = d_fake.mean() - d_real.mean()
             if self.gp:
                 loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
+            if self.dsync is not None and not self._capturing:
+                self.dsync.begin()
             (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
 
