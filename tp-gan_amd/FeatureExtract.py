@@ -70,10 +70,31 @@ class IdentityPreservingLoss(nn.Module):
             p.requires_grad_(False)
         self.compute_dtype = compute_dtype
 
-    def forward(self, fake, real):
+    def real_features_async(self, real):
+        """Start the real images' features (they do not depend on G) on a side HIP stream,
+        planned for a share of the chip, so that they run under G's forward; the handle goes
+        to forward(pre=...).  None when there is no GPU side stream to use."""
+        if not (tpgan_ops.MULTISTREAM and real.is_cuda):
+            return None
+        main = torch.cuda.current_stream()
+        st = tpgan_ops.side_streams(real.device, 1)[0]
+        st.wait_stream(main)
+        with torch.cuda.stream(st), torch.no_grad(), tpgan_ops.compute_dtype(self.compute_dtype), \
+                tpgan_ops.concurrent():
+            fr = self.extractor.extract_features(real)
+        return st, fr
+
+    def forward(self, fake, real, pre=None):
         with tpgan_ops.compute_dtype(self.compute_dtype):
-            with torch.no_grad():
-                fr = self.extractor.extract_features(real)
+            if pre is not None:
+                st, fr = pre
+                main = torch.cuda.current_stream()
+                main.wait_stream(st)
+                for t in fr:
+                    t.record_stream(main)
+            else:
+                with torch.no_grad():
+                    fr = self.extractor.extract_features(real)
             ff = self.extractor.extract_features(fake)
         loss = 0.0
         for a, b in zip(ff, fr):

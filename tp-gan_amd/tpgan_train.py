@@ -378,6 +378,9 @@ class TPGANTrainer:
         G, D = self.G, self.D
         self.fG.zero_grad()
         self.fD.zero_grad()
+        # the identity loss's real-image features run on a side stream under G's forward
+        pre = getattr(self.identity_fn, "real_features_async", None)
+        self._id_pre = pre(b["frontal"]) if pre is not None else None
         with tpgan_ops.compute_dtype(self.dtype):
             outs = G(b["I128"], b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], self.use_dropout)
             fake = outs[0]
@@ -433,7 +436,12 @@ class TPGANTrainer:
                   w["weight_symmetry"] * l_sym + w["weight_adv_G"] * l_adv + w["weight_total_varation"] * l_tv +
                   w["weight_cross_entropy"] * l_ce)
         if self.identity_fn is not None:
-            loss_G = loss_G + w["weight_identity_preserving"] * self.identity_fn(f32, front)
+            if self._id_pre is not None:
+                l_ip = self.identity_fn(f32, front, pre=self._id_pre)
+                self._id_pre = None
+            else:
+                l_ip = self.identity_fn(f32, front)
+            loss_G = loss_G + w["weight_identity_preserving"] * l_ip
         if self.gsync is not None and not self._capturing:
             self.gsync.begin()
         (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
