@@ -11,8 +11,9 @@ TP-GAN identity-preserving loss uses (a build choice: the ref
 defines none): the input of the first SSD scale (bottleneck 12, 96 ch at H/16) and the
 conv2 output (1280 ch at H/32), MobileNetV2.py:200-206.
 
-The SSD landmark loss / decoder (MultiTaskLoss, MultiTaskDecoder, :342-649) belong to the
-landmark pretraining loop and are not part of this module yet.
+The SSD landmark pretraining pieces are at the end: the model's
+non_maximum_suppression / find_best_coordinates (:252-340) and MultiTaskLoss /
+MultiTaskDecoder (:342-649), batched tensor ops on the predictions' device.
 """
 import math
 
@@ -160,3 +161,178 @@ class MobileNetV2(nn.Module):
                 n = m.weight.size(1)
                 m.weight.data.normal_(0, 0.01)
                 m.bias.data.zero_()
+
+
+# ---- SSD landmark pretraining: NMS, target assignment loss and decoder ----
+# The reference (MobileNetV2.py:252-649) works on batch 1 with Python loops and .item() per
+# point.  Here every step is a tensor op on the predictions' device over the whole batch:
+# the distance matrix, per-landmark top-k thresholds and the nearest-landmark assignment of
+# each anchor are masks, the losses are masked sums; only greedy NMS keeps a loop, one
+# iteration per KEPT point (argmax of the remaining scores, then a vector suppression).
+# Repairs of reference crashes (numbered after SURVEY.md §0.6's R1-R5):
+#   R6  non_maximum_suppression (:285-286) indexes a 0-d tensor once exactly one point
+#       survives a round (IndexError); here the lone survivor is simply kept.
+#   R7  MultiTaskLoss (:507-510) squeezes a single background index to an int: index 0
+#       is then skipped and any other single index raises; here it is one background sample.
+
+
+def _greedy_nms(points, scores, threshold, max_keep=None):
+    """Indices of `points` kept by greedy NMS, highest score first: take the best remaining
+    point, drop every remaining point within `threshold` (Euclidean, <=), repeat."""
+    keep = []
+    if points.numel() == 0:
+        return torch.zeros(0, dtype=torch.long, device=points.device)
+    alive = torch.ones(points.shape[0], dtype=torch.bool, device=points.device)
+    neg = torch.finfo(scores.dtype).min
+    while bool(alive.any()) and (max_keep is None or len(keep) < max_keep):
+        i = torch.where(alive, scores, torch.full_like(scores, neg)).argmax()
+        keep.append(i)
+        d = torch.linalg.vector_norm(points - points[i], dim=1)
+        alive &= d > threshold
+        alive[i] = False
+    return torch.stack(keep) if keep else torch.zeros(0, dtype=torch.long, device=points.device)
+
+
+def _mnv2_nms(self, points, scores, distance_threshold):
+    """MobileNetV2.non_maximum_suppression (:252-288): kept indices (list), best first (R6)."""
+    if points.numel() == 0:
+        return []
+    return [int(i) for i in _greedy_nms(points, scores, distance_threshold)]
+
+
+def _mnv2_best_coordinates(self, locations, classifications, distance_threshold=15.0):
+    """MobileNetV2.find_best_coordinates (:290-340): per landmark, the mean of the NMS
+    survivors of batch element 0 (locations (B, N, 10), classifications (B, N, 5))."""
+    names = ("lefteye", "righteye", "nose", "leftmouth", "rightmouth")
+    out = {}
+    for j, name in enumerate(names):
+        pts = locations[0, :, 2 * j:2 * j + 2]
+        keep = _greedy_nms(pts, classifications[0, :, j], distance_threshold)
+        out[name] = pts[keep].mean(dim=0)
+    return out
+
+
+MobileNetV2.non_maximum_suppression = _mnv2_nms
+MobileNetV2.find_best_coordinates = _mnv2_best_coordinates
+
+
+class MultiTaskLoss(nn.Module):
+    """SSD landmark loss (MobileNetV2.py:342-534): alpha * location MSE + beta * class CE.
+
+    Target assignment per image: d = cdist(anchors, 4 landmarks); landmark l's positives are
+    the anchors with d <= the k-th smallest distance to l (k = int(ratio * n)); an anchor
+    positive for several landmarks takes the nearest (the first on ties), the rest are
+    background (class 4).  Location loss: per landmark, the MSE between its positives and
+    the landmark, both divided by (width, height) and clamped to [0, 1]; class loss: CE of
+    the background samples (at most ratio_non_background x #positives, drawn uniformly
+    without replacement when there are more) plus, per landmark, CE of its positives.  The
+    reference takes batch 1; a batch here is the mean of the per-image losses.  `verbose`
+    prints the reference's per-term lines (:488, 516, 527)."""
+
+    def __init__(self, alpha=None, beta=None, distance_threshold_ratio=0.1, ratio_non_background=None,
+                 verbose=False):
+        super(MultiTaskLoss, self).__init__()
+        from config import pretrain
+        self.alpha = pretrain["loss"]["alpha"] if alpha is None else alpha
+        self.beta = pretrain["loss"]["beta"] if beta is None else beta
+        self.distance_threshold_ratio = distance_threshold_ratio
+        self.ratio_non_background = (pretrain["loss"]["ratio_non_background"] if ratio_non_background is None
+                                     else ratio_non_background)
+        self.verbose = verbose
+
+    def get_positive_samples_and_classification_tensor(self, locations_pred, locations_true):
+        """(positive index lists per landmark of image 0, labels (B, n) int: landmark or -1)."""
+        B, n, _ = locations_pred.shape
+        true = locations_true.reshape(B, 4, 2).to(locations_pred.dtype)
+        d = torch.cdist(locations_pred, true, p=2)                       # (B, n, 4)
+        k = int(self.distance_threshold_ratio * n)
+        if k < 1:
+            raise ValueError("distance_threshold_ratio * anchors < 1: no positives can be chosen")
+        thr = d.topk(k, dim=1, largest=False)[0].amax(dim=1, keepdim=True)  # (B, 1, 4)
+        pos = d <= thr
+        dm = torch.where(pos, d, torch.full_like(d, float("inf")))
+        labels = torch.where(pos.any(dim=2), dm.argmin(dim=2), torch.full_like(dm[..., 0], -1, dtype=torch.long))
+        lists = [torch.nonzero(labels[0] == l).flatten().tolist() for l in range(4)]
+        return lists, labels.to(torch.int32)
+
+    def forward(self, locations_pred, classifications_pred, locations_true, image_size):
+        B, n, _ = locations_pred.shape
+        _, labels = self.get_positive_samples_and_classification_tensor(locations_pred, locations_true)
+        labels = labels.long()
+        height, width = image_size
+        size = torch.tensor([width, height], device=locations_pred.device, dtype=locations_pred.dtype)
+        pred = torch.clamp(locations_pred / size, 0, 1)
+        true = torch.clamp(locations_true.reshape(B, 4, 2).to(locations_pred.dtype) / size, 0, 1)
+        onehot = labels.unsqueeze(2) == torch.arange(4, device=labels.device)       # (B, n, 4)
+        cnt = onehot.sum(dim=1)                                                      # (B, 4)
+        se = ((pred.unsqueeze(2) - true.unsqueeze(1)) ** 2).sum(dim=3)               # (B, n, 4)
+        present = cnt > 0
+        loc_l = torch.where(present, (se * onehot).sum(dim=1) / (2 * cnt.clamp(min=1)), torch.zeros_like(se[:, 0]))
+        # background: all of them, or a uniform draw without replacement of
+        # int(ratio * #positives) when there are more (random keys ranked among the background)
+        bg = labels == -1
+        nbg = bg.sum(dim=1, keepdim=True)
+        cap = ((n - nbg).to(torch.float64) * self.ratio_non_background).floor().long()
+        keys = torch.where(bg, torch.rand(bg.shape, device=bg.device), torch.full(bg.shape, 2.0, device=bg.device))
+        rank = keys.argsort(dim=1).argsort(dim=1)
+        sel = bg & ((nbg <= cap) | (rank < cap))
+        cp = classifications_pred if classifications_pred.dtype in (torch.float32, torch.float64) \
+            else classifications_pred.float()
+        logp = torch.log_softmax(cp, dim=2)                                          # (B, n, C)
+        nsel = sel.sum(dim=1)
+        cls_bg = torch.where(nsel > 0, -(logp[..., 4] * sel).sum(dim=1) / nsel.clamp(min=1), torch.zeros_like(nsel,
+                                                                                                       dtype=logp.dtype))
+        ce_l = -(logp[..., :4] * onehot).sum(dim=1)                                  # (B, 4)
+        cls_l = torch.where(present, ce_l / cnt.clamp(min=1), torch.zeros_like(ce_l))
+        loc = loc_l.sum(dim=1)
+        cls = cls_bg + cls_l.sum(dim=1)
+        if self.verbose:
+            for l in range(4):
+                if bool(present[0, l]):
+                    print("location loss %d               : %.4f * %s = %.4f" % (l, float(loc_l[0, l]), self.alpha,
+                                                                                 float(loc_l[0, l]) * self.alpha))
+            if int(nsel[0]):
+                print("background classification loss: %.4f * %s = %.4f" % (float(cls_bg[0]), self.beta,
+                                                                            float(cls_bg[0]) * self.beta))
+            for l in range(4):
+                if bool(present[0, l]):
+                    print("classification loss %d         : %.4f * %s = %.4f" % (l, float(cls_l[0, l]), self.beta,
+                                                                                 float(cls_l[0, l]) * self.beta))
+        total = self.alpha * loc + self.beta * cls.to(loc.dtype)
+        return total.mean()
+
+
+class MultiTaskDecoder(nn.Module):
+    """SSD landmark decoder (MobileNetV2.py:536-649): per image and class, the anchors whose
+    softmax confidence exceeds confidence_threshold, greedy NMS at nms_distance_threshold
+    pixels, at most top_k of them; a list per image of (class, score, point) tuples."""
+
+    def __init__(self, confidence_threshold=0.5, top_k=1, nms_distance_threshold=20):
+        super(MultiTaskDecoder, self).__init__()
+        self.confidence_threshold = confidence_threshold
+        self.top_k = top_k
+        self.nms_distance_threshold = nms_distance_threshold
+
+    def forward(self, locations, classifications):
+        scores = torch.softmax(classifications, dim=-1)
+        output = []
+        for i in range(locations.shape[0]):
+            results = []
+            for c in range(scores.shape[2]):
+                s = scores[i, :, c]
+                mask = s > self.confidence_threshold
+                if not bool(mask.any()):
+                    continue
+                pts, sc = locations[i][mask], s[mask]
+                keep = _greedy_nms(pts, sc, self.nms_distance_threshold, max_keep=self.top_k)
+                for j in keep:
+                    results.append((c, sc[j], pts[j]))
+            output.append(results)
+        return output
+
+    def nms(self, locations, scores):
+        """Kept indices (tensor), best first (MobileNetV2.py:599-636)."""
+        return _greedy_nms(locations, scores, self.nms_distance_threshold).cpu()
+
+    def euclidean_distance(self, point1, points2):
+        return torch.linalg.vector_norm(points2 - point1, dim=1)
