@@ -184,9 +184,10 @@ def main():
         with open(pmc) as f:
             pj = json.load(f)
         traffic = int(pj["traffic_bytes"])
-        traffic_src = ("profiles/pmc_dominant.json: rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, median per "
-                       "dispatch of tools/bench_layers.py enhance_128 fwd; algorithmic %d B (x, residual in, y out, "
-                       "weights)" % int(pj.get("algorithmic_bytes", 0)))
+        traffic_src = ("profiles/pmc_dominant.json: rocprofv3 --pmc FETCH_SIZE (x2, calibrated) + WRITE_SIZE "
+                       "(exact, calibrated), median over the forward-only dispatches (grid filter) of "
+                       "tools/bench_layers.py enhance_128; algorithmic %d B (x, residual in, y out, weights)"
+                       % int(pj.get("algorithmic_bytes", 0)))
     workload = "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, 128x128, bf16"
     ext_name = {"resnet50": "ResNet-50", "mobilenetv2": "MobileNetV2"}.get(args.identity)
     if args.config == 5:

@@ -14,6 +14,8 @@ $P --pmc FETCH_SIZE -d $O/e128_fetch -o run -- $BL --only enhance_128 --passes f
 $P --pmc WRITE_SIZE -d $O/e128_write -o run -- $BL --only enhance_128 --passes fwd > $O/e128_write.log 2>&1
 $P --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum -d $O/e128_wrreq -o run -- $BL --only enhance_128 --passes fwd > $O/e128_wrreq.log 2>&1
 $P --pmc WRITE_SIZE -d $O/c0_write -o run -- $BL --only conv0_res --passes fwd > $O/c0_write.log 2>&1
+$P --pmc FETCH_SIZE -d $O/wg_fetch -o run -- $BL --only enhance_128 --passes wgrad > $O/wg_fetch.log 2>&1
+$P --pmc WRITE_SIZE -d $O/wg_write -o run -- $BL --only enhance_128 --passes wgrad > $O/wg_write.log 2>&1
 echo traffic done
 for pass in fwd dgrad wgrad; do
   $P --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS \

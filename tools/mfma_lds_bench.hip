@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <type_traits>
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -21,14 +22,14 @@ __device__ __forceinline__ f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
 // MODE 0: all reads, then the MFMAs (hipcc's waits; sched_group_barrier as the halo kernel)
 // MODE 1: no LDS reads in the loop (fragments from registers): the MFMA + barrier floor
 // MODE 2: all reads, then each column waits for its own B fragment (inline asm, counted)
-template <int MREP, int NREP, int MODE, int BARP, int DMA>
-__global__ __launch_bounds__(512) void loop_kernel(int taps, float* out, const char* wsrc) {
+template <int MREP, int NREP, int MODE, int BARP, int DMA, int NW = 8>
+__global__ __launch_bounds__(NW * 64) void loop_kernel(int taps, float* out, const char* wsrc) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
   u32x4* A = lds;              // halo: 1024 rows x 4 chunks (64 KiB)
   u32x4* B = lds + 4096;       // 3 slots x 256 rows x 4 chunks (48 KiB)
-  for (int i = tid; i < 4096 + 3072; i += 512) lds[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
+  for (int i = tid; i < 4096 + 3072; i += NW * 64) lds[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
   __syncthreads();
   f32x4 acc[MREP][NREP];
 #pragma unroll
@@ -56,20 +57,51 @@ __global__ __launch_bounds__(512) void loop_kernel(int taps, float* out, const c
       xb[set][n] = B[(t % 3) * 1024 + r * 4 + (g ^ (((r >> 2) & 1) << 1))];
     }
   };
-  if constexpr (MODE == 3) rd(0, 0);
-  for (int t = 0; t < taps; ++t) {
-    const int shift = (t % 5) + 68 * ((t / 5) % 5);  // 5x5 taps over a 68-wide halo
-    const int slot = t % 3;
-    if constexpr (MODE == 3) {
-      const int cur = t & 1;
+  constexpr bool ILV = MODE == 4;
+  if constexpr (MODE == 3 || MODE == 4) {
+    // two taps per iteration so that the register sets are compile-time indices
+    rd(0, 0);
+    auto step = [&](int t, auto CUR) {
+      constexpr int cur = decltype(CUR)::value;
       if (t + 1 < taps) rd(t + 1, cur ^ 1);
 #pragma unroll
       for (int n = 0; n < NREP; ++n)
 #pragma unroll
         for (int m = 0; m < MREP; ++m) acc[m][n] = mma(xa[cur][m], xb[cur][n], acc[m][n]);
-      __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP, 0);
-    } else if constexpr (MODE == 1) {
+      if constexpr (ILV) {  // one next-tap read after each column's MFMAs
+#pragma unroll
+        for (int n = 0; n < NREP; ++n) {
+          __builtin_amdgcn_sched_group_barrier(0x008, MREP, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, MREP, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP, 0);
+      }
+      if constexpr (DMA > 0) {
+        char* dst = reinterpret_cast<char*>(B + ((t + 2) % 3) * 1024) + wave * DMA * 1024;
+        const char* src = wsrc + ((t * 7) % 64) * 16384 + (wave * DMA * 1024 + lane * 16);
+#pragma unroll
+        for (int j = 0; j < DMA; ++j)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j * 1024),
+                                           (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, 0, 0);
+      }
+      if constexpr (DMA == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if constexpr (DMA == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if constexpr (DMA == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    for (int t = 0; t < taps; t += 2) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+    }
+    taps = 0;  // (the generic loop below is skipped)
+  }
+  for (int t = 0; t < taps; ++t) {
+    const int shift = (t % 5) + 68 * ((t / 5) % 5);  // 5x5 taps over a 68-wide halo
+    const int slot = t % 3;
+    if constexpr (MODE == 1) {
 #pragma unroll
       for (int n = 0; n < NREP; ++n)
 #pragma unroll
@@ -137,7 +169,8 @@ __global__ __launch_bounds__(512) void loop_kernel(int taps, float* out, const c
     }
     if constexpr (BARP > 0) {
       if ((t % BARP) == BARP - 1) {
-        if constexpr (DMA == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (DMA == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if constexpr (DMA == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else if constexpr (DMA == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
@@ -149,24 +182,24 @@ __global__ __launch_bounds__(512) void loop_kernel(int taps, float* out, const c
   for (int m = 0; m < MREP; ++m)
 #pragma unroll
     for (int n = 0; n < NREP; ++n) s += acc[m][n][0];
-  out[blockIdx.x * 512 + tid] = s;
+  out[blockIdx.x * 512 + tid] = s;  // (NW <= 8)
 }
 
-template <int MREP, int NREP, int MODE, int BARP, int DMA = 0>
+template <int MREP, int NREP, int MODE, int BARP, int DMA = 0, int NW = 8>
 static int run(const char* name, float* out, int taps, hipEvent_t e0, hipEvent_t e1, const char* w) {
-  auto k = loop_kernel<MREP, NREP, MODE, BARP, DMA>;
+  auto k = loop_kernel<MREP, NREP, MODE, BARP, DMA, NW>;
   const int lds = 150 * 1024;  // one block per CU
   CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   const int blocks = 256 * 4;
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, 0, taps, out, w);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(NW * 64), lds, 0, taps, out, w);
   CHECK(hipEventRecord(e0));
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, 0, taps, out, w);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(NW * 64), lds, 0, taps, out, w);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
-  const double flops = 2.0 * 16 * 16 * 32 * MREP * NREP * 8.0 * taps * blocks;
-  printf("%-34s bar/%d dma %d MREP %d NREP %2d  %.3f ms  %.0f TF/s  %.1f %% of 2.5 PF\n", name, BARP, DMA, MREP, NREP, ms, flops / ms / 1e9,
+  const double flops = 2.0 * 16 * 16 * 32 * MREP * NREP * (double)NW * taps * blocks;
+  printf("%-26s %dw bar/%d dma %d MREP %d NREP %2d  %.3f ms  %.0f TF/s  %.1f %% of 2.5 PF\n", name, NW, BARP, DMA, MREP, NREP, ms, flops / ms / 1e9,
          flops / ms / 1e9 / 25.0);
   return 0;
 }
@@ -182,6 +215,16 @@ int main() {
   CHECK(hipMalloc(&w, 64 * 16384 + 65536));
   CHECK(hipMemset(w, 0, 64 * 16384 + 65536));
   run<2, 13, 1, 1>("regs only", out, taps, e0, e1, w);
+  run<4, 7, 1, 1, 0, 4>("regs only", out, taps, e0, e1, w);
+  run<4, 7, 0, 1, 0, 4>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<4, 7, 0, 1, 4, 4>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<4, 7, 4, 1, 4, 4>("prefetch interleaved", out, taps, e0, e1, w);
+  run<4, 13, 0, 1, 4, 4>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<4, 13, 4, 1, 4, 4>("prefetch interleaved", out, taps, e0, e1, w);
+  run<2, 13, 4, 1, 2>("prefetch interleaved", out, taps, e0, e1, w);
+  run<4, 7, 4, 1, 2>("prefetch interleaved", out, taps, e0, e1, w);
+  run<4, 4, 4, 1, 1>("prefetch interleaved", out, taps, e0, e1, w);
+  run<2, 13, 4, 1, 0>("prefetch interleaved", out, taps, e0, e1, w);
   run<2, 13, 3, 1, 2>("prefetch next tap", out, taps, e0, e1, w);
   run<4, 7, 3, 1, 2>("prefetch next tap", out, taps, e0, e1, w);
   run<4, 4, 3, 1, 1>("prefetch next tap", out, taps, e0, e1, w);
