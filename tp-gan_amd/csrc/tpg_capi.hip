@@ -249,27 +249,9 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   const int sy = dymax - dymin + 1, sx = dxmax - dxmin + 1;
   if (sy > 7 || sx > 7) return;
   const int JH = a.JH, JW = a.JW;
-  const int HCAP = 5 * 128;
-  int bth = 0, btw = 0, bimg = 0;
-  int64_t bcost = -1;
-  auto consider = [&](int th, int tw, int img) {
-    if (th < 1 || tw < 1 || img < 1 || th * tw * img > 256) return;
-    const int hpi = (th + sy - 1) * (tw + sx - 1);
-    if ((int64_t)img * hpi > HCAP) return;
-    const int64_t nsub = (int64_t)N * cdiv(JH, th) * cdiv(JW, tw);
-    const int64_t blocks = (nsub + img - 1) / img;
-    const int64_t cost = blocks * (256 * (int64_t)a.ntaps + (int64_t)img * hpi);
-    if (bcost < 0 || cost < bcost) { bcost = cost; bth = th; btw = tw; bimg = img; }
-  };
-  if (JH * JW <= 256)
-    for (int img = std::min(256 / (JH * JW), N); img >= 1; --img) consider(JH, JW, img);
-  for (int tw : {JW, 64, 48, 40, 32, 24, 16, 8}) {
-    if (tw > JW || tw > 256) continue;
-    const int thmax = std::min(JH, 256 / tw);
-    if (thmax < 1) continue;
-    consider(cdiv(JH, cdiv(JH, thmax)), tw, 1);
-  }
-  if (bcost < 0) return;
+  // output channels per block first: the 512-row tile (halo up to 1024 pixels) serves the
+  // thin layers (BN 64 / 80) of the large maps, where 256 rows run only 8-10 MFMAs per wave
+  // between tap barriers; it needs >= 512 blocks (two rounds of the chip) without a k split
   int bn;
   if (a.Nout <= 32) bn = 32;
   else if (a.Nout <= 64) bn = 64;
@@ -288,11 +270,39 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
       if (best < 0 || pad < best) { best = pad; bn = c; }
     }
   }
+  static const bool no512 = getenv("TPG_HALO_NO512") != nullptr;  // (A/B hook)
+  // (not for deep inputs: conv5_0's 206 -> 64 forward measured 0.43 -> 0.46 ms with it, against
+  // add_128 0.59 -> 0.49 and conv0_res 0.35 -> 0.27)
+  const int bm = (!no512 && halo_cfg512(bn) >= 0 && dtype != TPG_F32 && (int64_t)N * JH * JW >= 512 * 512 &&
+                  JW >= 64 && cdiv(a.Nout, bn) == 1 && a.C <= 128) ? 512 : 256;
+  const int HCAP = bm == 512 ? 1024 : 5 * 128;
+  int bth = 0, btw = 0, bimg = 0;
+  int64_t bcost = -1;
+  auto consider = [&](int th, int tw, int img) {
+    if (th < 1 || tw < 1 || img < 1 || th * tw * img > bm) return;
+    const int hpi = (th + sy - 1) * (tw + sx - 1);
+    if ((int64_t)img * hpi > HCAP) return;
+    const int64_t nsub = (int64_t)N * cdiv(JH, th) * cdiv(JW, tw);
+    const int64_t blocks = (nsub + img - 1) / img;
+    const int64_t cost = blocks * ((int64_t)bm * a.ntaps + (int64_t)img * hpi);
+    if (bcost < 0 || cost < bcost) { bcost = cost; bth = th; btw = tw; bimg = img; }
+  };
+  if (JH * JW <= bm)
+    for (int img = std::min(bm / (JH * JW), N); img >= 1; --img) consider(JH, JW, img);
+  for (int tw : {JW, 64, 48, 40, 32, 24, 16, 8}) {
+    if (tw > JW || tw > bm) continue;
+    const int thmax = std::min(JH, bm / tw);
+    if (thmax < 1) continue;
+    consider(cdiv(JH, cdiv(JH, thmax)), tw, 1);
+  }
+  if (bcost < 0) return;
+  if (a.Nout <= 32) bn = 32;
+  else if (a.Nout <= 64) bn = 64;
   // (whole 16-pixel rows: the masked-gradient mode DMAs y into the halo buffer 16 pixels per
   // wave instruction)
   const int hcap = (int)rup((int64_t)bimg * (bth + sy - 1) * (btw + sx - 1), 16);
   const int hl = std::max(3, cdiv(hcap * 4, 512));
-  const int cfg = halo_cfg(hl, bn);
+  const int cfg = bm == 512 ? halo_cfg512(bn) : halo_cfg(hl, bn);
   if (cfg < 0) return;
   HaloArgs& h = P.h;
   memset(&h, 0, sizeof(h));

@@ -37,7 +37,8 @@ __device__ __forceinline__ int hswz(int row) { return ((row >> 2) & 1) << 1; }
 __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 128; }
 // epilogue: rows of the 256-row tile parked in LDS per pass (fp32, stride BN + 4)
 __host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 80 ? 128 : 256; }
-__host__ __device__ constexpr int halo_epi_lds(int bn) { return 256 * 20 + halo_epi_rows(bn) * (bn + 4) * 4; }
+// (row-offset table [BM][2] int64 + bias [256] floats, then the parked accumulator rows)
+__host__ __device__ constexpr int halo_epi_lds(int bn, int bm = 256) { return bm * 16 + 1024 + halo_epi_rows(bn) * (bn + 4) * 4; }
 
 // mask_chunk on a native 4 x u32 vector (first-class value: stays in VGPRs)
 template <int EPC>
@@ -73,13 +74,14 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
   return a.u;
 }
 
-template <int DT, int HL, int BN, int WM, int WN, bool MASK>
+template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256>
 __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   using E = dt_t<DT>;
   constexpr bool BF = DT != 0;  // 16-bit operands (bf16 or fp16)
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
   constexpr int KS = 4 * EPC;                // channels per 64-byte step
-  constexpr int BM = 256;                    // output rows per block (IMG sub-tiles)
+  // BM output rows per block (IMG sub-tiles): 256, or 512 for the thin (<= 80-channel) layers
+  // of the large maps, which then run 2x the MFMAs per tap barrier
   constexpr int BNL = halo_bnl(BN);          // weight rows per LDS slot (multiple of 128)
   constexpr int GL = BNL / 128;              // 1 KiB LDS-DMA pieces per wave per step
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -397,14 +399,13 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   constexpr int NV = 8 * (int)sizeof(E) / 16;  // 16-byte vectors per group
   static_assert(RP % WTM == 0, "epilogue tiling");
   __syncthreads();                           // every wave is done with the halo and the ring
-  int64_t* s_off = reinterpret_cast<int64_t*>(lds);           // [256][2] out / residual offsets
-  float* s_bias = reinterpret_cast<float*>(lds) + 256 * 4;    // [256] bias of this block's columns
-  float* s_acc = reinterpret_cast<float*>(lds) + 256 * 5;     // [RP][LDW]
+  int64_t* s_off = reinterpret_cast<int64_t*>(lds);           // [BM][2] out / residual offsets
+  float* s_bias = reinterpret_cast<float*>(lds) + BM * 4;     // [256] bias of this block's columns
+  float* s_acc = reinterpret_cast<float*>(lds) + BM * 4 + 256;  // [RP][LDW]
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
   float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
-  if (tid < BM) {
-    const int q = tid;
+  for (int q = tid; q < BM; q += 512) {
     const int sub = q / THW, rem = q - sub * THW;
     const int st = st0 + sub;
     int64_t yo = -1, ro = 0;
@@ -425,9 +426,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
     }
     s_off[2 * q] = yo;
     s_off[2 * q + 1] = ro;
-  } else if (tid < BM + BN) {
-    const int c = n0 + tid - BM;
-    s_bias[tid - BM] = (p.bias && c < p.Nout) ? p.bias[c] : 0.f;
+  }
+  if (tid >= 512 - BN) {  // (the highest threads: BM >= 256 > BN)
+    const int c = n0 + tid - (512 - BN);
+    s_bias[tid - (512 - BN)] = (p.bias && c < p.Nout) ? p.bias[c] : 0.f;
   }
 #pragma unroll 1
   for (int pass = 0; pass < BM / RP; ++pass) {
@@ -545,6 +547,12 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   TPG_HALO_BN(X, 0, 3)          \
   TPG_HALO_BN(X, 8, 4)          \
   TPG_HALO_BN(X, 16, 5)
+// 512-row tiles (ids 24, 25): BN 64 / 80 on the large maps, halo up to 1024 pixels
+#define TPG_HALO_CFGS512(X)     \
+  X(24, 8, 64, 8, 1)            \
+  X(25, 8, 80, 8, 1)
+
+int halo_cfg512(int bn) { return bn == 64 ? 24 : bn == 80 ? 25 : -1; }
 
 int halo_cfg(int hl, int bn) {
   const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : bn == 208 ? 5
@@ -556,15 +564,15 @@ int halo_cfg(int hl, int bn) {
 // Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
 // 7x7 layers alone, -2 % on the train step) and a cross-barrier fragment prefetch with a
 // 4-slot ring (-2..12 %: the second fragment set pushed the 224-wide tile past 256 VGPRs).
-size_t halo_lds_bytes(int hcap, int bn, int rs) {
-  return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn));
+size_t halo_lds_bytes(int hcap, int bn, int rs, int bm) {
+  return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn, bm));
 }
 
-template <int DT, int HL, int BN, int WM, int WN, bool MASK>
+template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256>
 static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
-  auto k = halo_kernel<DT, HL, BN, WM, WN, MASK>;
-  const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3);
-  const int maxl = (int)halo_lds_bytes(HL * 128, BN, 4);
+  auto k = halo_kernel<DT, HL, BN, WM, WN, MASK, BM>;
+  const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3, BM);
+  const int maxl = (int)halo_lds_bytes(HL * 128, BN, BM == 512 ? 3 : 4, BM);  // (512: 3-slot ring only)
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
                       true);
   (void)once;
@@ -588,6 +596,15 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
                       : launch_halo_t<0, HL_, BN_, WM_, WN_, false>(a, grid, s);           \
   }
   TPG_HALO_CFGS(X)
+#undef X
+#define X(id, HL_, BN_, WM_, WN_)                                                          \
+  if (cfg == (id)) {                                                                       \
+    if (a.hcap > HL_ * 128 || mask || (a.var & 2)) return -1;                              \
+    return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, false, 512>(a, grid, s)       \
+         : dtype == 2 ? launch_halo_t<2, HL_, BN_, WM_, WN_, false, 512>(a, grid, s)       \
+                      : launch_halo_t<0, HL_, BN_, WM_, WN_, false, 512>(a, grid, s);      \
+  }
+  TPG_HALO_CFGS512(X)
 #undef X
   return -1;
 }

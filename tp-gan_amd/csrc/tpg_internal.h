@@ -362,7 +362,8 @@ int launch_epilogue(const EpiArgs& a, hipStream_t s);
 int launch_wgrad_rh(const WgradRHArgs& a, hipStream_t s);
 int wgrad_rh_tile(int cfg, int* bm, int* bc);
 int halo_cfg(int hl, int bn);
-size_t halo_lds_bytes(int hcap, int bn, int rs = 3);
+size_t halo_lds_bytes(int hcap, int bn, int rs = 3, int bm = 256);
+int halo_cfg512(int bn);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask = false);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
