@@ -39,6 +39,10 @@ SHAPES = {
     "local_20": (32, 128, 20, 20, 128, 3, 1, 1, False, 0, ACT_LEAKY, True),
     "local_40": (32, 64, 40, 40, 64, 3, 1, 1, False, 0, ACT_LEAKY, True),
     "conv4_s2": (32, 256, 16, 16, 512, 3, 2, 1, False, 0, ACT_LEAKY, False),
+    "conv1_s2": (32, 64, 128, 128, 64, 5, 2, 2, False, 0, ACT_LEAKY, False),
+    "conv2_s2": (32, 64, 64, 64, 128, 3, 2, 1, False, 0, ACT_LEAKY, False),
+    "conv3_s2": (32, 128, 32, 32, 256, 3, 2, 1, False, 0, ACT_LEAKY, False),
+    "d_conv1_s2": (64, 64, 64, 64, 128, 3, 2, 1, False, 0, ACT_LEAKY, False),
 }
 
 

@@ -238,9 +238,12 @@ static int32_t check_desc(const tpg_conv_desc* d) {
 // of one image (large maps) or IMG whole images per 256-row block (small maps), minimising
 // computed rows x taps plus staged halo pixels; then a split over k-steps when the grid
 // has too few blocks to fill the chip (fp32 partial slices, summed by the epilogue).
-static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
+static void maybe_halo(Prob& P, int dtype, int N) {
   IgemmArgs& a = P.a;
-  if (!unit_stride || a.ntaps < 1 || a.C < 1) return;
+  // unit-stride grids, and stride 2 in both directions (halo (2·th + k − 2) x (2·tw + k − 2))
+  const int S = a.ist_h;
+  static const bool no_s2 = getenv("TPG_HALO_NO_S2") != nullptr;  // (A/B hook)
+  if (a.ntaps < 1 || a.C < 1 || a.ist_h != a.ist_w || (S != 1 && (S != 2 || no_s2))) return;
   int dymin = 127, dymax = -128, dxmin = 127, dxmax = -128;
   for (int t = 0; t < a.ntaps; ++t) {
     dymin = std::min<int>(dymin, a.dy[t]); dymax = std::max<int>(dymax, a.dy[t]);
@@ -273,14 +276,15 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   static const bool no512 = getenv("TPG_HALO_NO512") != nullptr;  // (A/B hook)
   // (not for deep inputs: conv5_0's 206 -> 64 forward measured 0.43 -> 0.46 ms with it, against
   // add_128 0.59 -> 0.49 and conv0_res 0.35 -> 0.27)
-  const int bm = (!no512 && halo_cfg512(bn) >= 0 && dtype != TPG_F32 && (int64_t)N * JH * JW >= 512 * 512 &&
+  if (S == 2 && bn > 128) bn = 128;  // (the 1024-pixel halo leaves LDS for 128-row weight slices)
+  const int bm = (!no512 && S == 1 && halo_cfg512(bn) >= 0 && dtype != TPG_F32 && (int64_t)N * JH * JW >= 512 * 512 &&
                   JW >= 64 && cdiv(a.Nout, bn) == 1 && a.C <= 128) ? 512 : 256;
-  const int HCAP = bm == 512 ? 1024 : 5 * 128;
+  const int HCAP = (bm == 512 || S == 2) ? 1024 : 5 * 128;
   int bth = 0, btw = 0, bimg = 0;
   int64_t bcost = -1;
   auto consider = [&](int th, int tw, int img) {
     if (th < 1 || tw < 1 || img < 1 || th * tw * img > bm) return;
-    const int hpi = (th + sy - 1) * (tw + sx - 1);
+    const int hpi = ((th - 1) * S + sy) * ((tw - 1) * S + sx);
     if ((int64_t)img * hpi > HCAP) return;
     const int64_t nsub = (int64_t)N * cdiv(JH, th) * cdiv(JW, tw);
     const int64_t blocks = (nsub + img - 1) / img;
@@ -294,15 +298,18 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
     const int thmax = std::min(JH, bm / tw);
     if (thmax < 1) continue;
     consider(cdiv(JH, cdiv(JH, thmax)), tw, 1);
+    // (stride 2: the tallest tile's halo may not fit; shorter ones, whole rows per block)
+    if (S > 1)
+      for (int th = thmax - 1; th >= 1 && th * tw * 2 >= bm / 2; --th) consider(th, tw, 1);
   }
   if (bcost < 0) return;
   if (a.Nout <= 32) bn = 32;
   else if (a.Nout <= 64) bn = 64;
   // (whole 16-pixel rows: the masked-gradient mode DMAs y into the halo buffer 16 pixels per
   // wave instruction)
-  const int hcap = (int)rup((int64_t)bimg * (bth + sy - 1) * (btw + sx - 1), 16);
+  const int hcap = (int)rup((int64_t)bimg * ((bth - 1) * S + sy) * ((btw - 1) * S + sx), 16);
   const int hl = std::max(3, cdiv(hcap * 4, 512));
-  const int cfg = bm == 512 ? halo_cfg512(bn) : halo_cfg(hl, bn);
+  const int cfg = bm == 512 ? halo_cfg512(bn) : halo_cfg(S == 2 ? 8 : hl, bn);
   if (cfg < 0) return;
   HaloArgs& h = P.h;
   memset(&h, 0, sizeof(h));
@@ -311,8 +318,8 @@ static void maybe_halo(Prob& P, int dtype, int N, bool unit_stride) {
   h.nks = cdiv(a.C, ks_elems);
   h.ntaps = a.ntaps;
   h.dymin = dymin; h.dxmin = dxmin;
-  h.TH = bth; h.TW = btw; h.IMG = bimg; h.SH = 1; h.SW = 1;
-  h.HH = bth + sy - 1; h.HW = btw + sx - 1;
+  h.TH = bth; h.TW = btw; h.IMG = bimg; h.SH = S; h.SW = S;
+  h.HH = (bth - 1) * S + sy; h.HW = (btw - 1) * S + sx;
   h.hcap = hcap;
   static const int halo_var = getenv("TPG_HALO_VAR") ? atoi(getenv("TPG_HALO_VAR")) : 0;  // tuning
   h.var = halo_var;
@@ -362,7 +369,7 @@ static std::vector<Prob> plan_fwd(const tpg_conv_desc* d, bool composite) {
       P.a.pad_mode = d->pad_mode;
       P.pk.nmode = 0; P.pk.cmode = 1;
       finish(P, d->dtype, d->n * d->out_h * d->out_w);
-      maybe_halo(P, d->dtype, d->n, d->stride_h == 1 && d->stride_w == 1);
+      maybe_halo(P, d->dtype, d->n);
       v.push_back(P);
     }
   } else {
@@ -378,7 +385,7 @@ static std::vector<Prob> plan_fwd(const tpg_conv_desc* d, bool composite) {
         P.a.C = d->in_c; P.a.A_H = d->in_h; P.a.A_W = d->in_w; P.a.Nout = d->out_c;
         P.pk.nmode = 1; P.pk.cmode = 0;
         finish(P, d->dtype, d->n * P.a.JH * P.a.JW);
-        maybe_halo(P, d->dtype, d->n, true);
+        maybe_halo(P, d->dtype, d->n);
         v.push_back(P);
       }
     }
@@ -419,7 +426,7 @@ static std::vector<Prob> plan_bwd_data(const tpg_conv_desc* d, bool composite) {
         P.a.C = d->out_c; P.a.A_H = d->out_h; P.a.A_W = d->out_w; P.a.Nout = d->in_c;
         P.pk.nmode = 1; P.pk.cmode = 0;
         finish(P, d->dtype, d->n * P.a.JH * P.a.JW);
-        maybe_halo(P, d->dtype, d->n, true);
+        maybe_halo(P, d->dtype, d->n);
         v.push_back(P);
       }
     }
@@ -436,7 +443,7 @@ static std::vector<Prob> plan_bwd_data(const tpg_conv_desc* d, bool composite) {
       P.a.C = d->out_c; P.a.A_H = d->out_h; P.a.A_W = d->out_w; P.a.Nout = d->in_c;
       P.pk.nmode = 0; P.pk.cmode = 1;
       finish(P, d->dtype, d->n * d->in_h * d->in_w);
-      maybe_halo(P, d->dtype, d->n, d->stride_h == 1 && d->stride_w == 1);
+      maybe_halo(P, d->dtype, d->n);
       v.push_back(P);
     }
   }

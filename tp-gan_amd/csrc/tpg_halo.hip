@@ -3,7 +3,8 @@
 // Covers every conv whose taps read the A grid with unit stride: Conv2d forward at
 // stride 1 (all 3x3 / 5x5 / 7x7 / 2x2-reflect layers of G and D), the Conv2d input
 // gradient at any stride and the ConvTranspose2d forward (one launch per parity class,
-// SURVEY.md §7 step 5).  That is > 90 % of the G+D train-step MACs of the fwd + dgrad passes.
+// SURVEY.md §7 step 5) — and, with SH = SW = 2 (output pixel (y, x) reads halo position
+// (2y, 2x) + tap), the stride-2 Conv2d forward and the ConvTranspose2d input gradient.
 //
 // Block = 256 output (sub-grid) pixels x BN output channels, 8 waves: one TH x TW tile of
 // one image, or IMG whole small images (8x8, 10x10, 5x5 ... maps) side by side.  K loop: for each 64-byte channel step (bf16: 32 ch, f32: 16 ch)
@@ -551,13 +552,22 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
 #define TPG_HALO_CFGS512(X)     \
   X(24, 8, 64, 8, 1)            \
   X(25, 8, 80, 8, 1)
+// stride-2 grids (ids 40..44): halo up to 1024 pixels, so only BN <= 128 fits LDS beside it
+#define TPG_HALO_CFGS_S2(X)     \
+  X(40, 8, 32, 8, 1)            \
+  X(41, 8, 64, 8, 1)            \
+  X(42, 8, 96, 8, 1)            \
+  X(43, 8, 128, 4, 2)           \
+  X(47, 8, 80, 8, 1)
 
 int halo_cfg512(int bn) { return bn == 64 ? 24 : bn == 80 ? 25 : -1; }
 
 int halo_cfg(int hl, int bn) {
   const int bi = bn == 32 ? 0 : bn == 64 ? 1 : bn == 96 ? 2 : bn == 128 ? 3 : bn == 224 ? 4 : bn == 208 ? 5
                : bn == 192 ? 6 : bn == 80 ? 7 : -1;
-  if (bi < 0 || hl < 3 || hl > 5) return -1;
+  if (bi < 0) return -1;
+  if (hl >= 6 && hl <= 8) return (bi <= 3 || bi == 7) ? 40 + bi : -1;  // (no mask mode)
+  if (hl < 3 || hl > 5) return -1;
   return 8 * (hl - 3) + bi;
 }
 
@@ -572,7 +582,7 @@ template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256>
 static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
   auto k = halo_kernel<DT, HL, BN, WM, WN, MASK, BM>;
   const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3, BM);
-  const int maxl = (int)halo_lds_bytes(HL * 128, BN, BM == 512 ? 3 : 4, BM);  // (512: 3-slot ring only)
+  const int maxl = (int)halo_lds_bytes(HL * 128, BN, HL == 8 ? 3 : 4, BM);  // (1024-pixel halos: 3-slot ring only)
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
                       true);
   (void)once;
@@ -605,6 +615,15 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
                       : launch_halo_t<0, HL_, BN_, WM_, WN_, false, 512>(a, grid, s);      \
   }
   TPG_HALO_CFGS512(X)
+#undef X
+#define X(id, HL_, BN_, WM_, WN_)                                                          \
+  if (cfg == (id)) {                                                                       \
+    if (a.hcap > HL_ * 128 || mask || (a.var & 2)) return -1;                              \
+    return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, false>(a, grid, s)            \
+         : dtype == 2 ? launch_halo_t<2, HL_, BN_, WM_, WN_, false>(a, grid, s)            \
+                      : launch_halo_t<0, HL_, BN_, WM_, WN_, false>(a, grid, s);           \
+  }
+  TPG_HALO_CFGS_S2(X)
 #undef X
   return -1;
 }
