@@ -43,6 +43,11 @@ SHAPES = {
     "conv2_s2": (32, 64, 64, 64, 128, 3, 2, 1, False, 0, ACT_LEAKY, False),
     "conv3_s2": (32, 128, 32, 32, 256, 3, 2, 1, False, 0, ACT_LEAKY, False),
     "d_conv1_s2": (64, 64, 64, 64, 128, 3, 2, 1, False, 0, ACT_LEAKY, False),
+    "local_s2": (32, 256, 10, 10, 512, 3, 2, 1, False, 0, ACT_LEAKY, False),
+    "local_up": (32, 512, 5, 5, 256, 3, 2, 1, True, 1, ACT_RELU, False),
+    "up_16": (32, 576, 8, 8, 512, 3, 2, 1, True, 1, ACT_RELU, False),
+    "up_64": (32, 416, 32, 32, 128, 3, 2, 1, True, 1, ACT_RELU, False),
+    "up_32": (32, 768, 16, 16, 256, 3, 2, 1, True, 1, ACT_RELU, False),
 }
 
 

@@ -138,7 +138,13 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
         const int hy = hl / HW, hx = hl - hy * HW;
         int gy = ty * TH * SH + p.dymin + hy, gx = tx * TW * SW + p.dxmin + hx;
         if (p.pad_mode) { gy = h_refl(gy, p.A_H); gx = h_refl(gx, p.A_W); }
-        if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W) {
+        bool real = true;
+        if (p.dil > 1) {  // zero-inserted grid: only multiples of dil are pixels of A
+          real = gy >= 0 && gx >= 0 && gy % p.dil == 0 && gx % p.dil == 0;
+          gy /= p.dil;
+          gx /= p.dil;
+        }
+        if (real && (unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W) {
           hoff[q] = (int)((int64_t)nimg * p.a_sn + gy * p.a_sh + gx * p.a_sw) + ch * EPC;
           if constexpr (MASK) {
             mpix[q] = (int)((int64_t)nimg * p.m_sn + gy * p.m_sh + gx * p.m_sw);

@@ -104,6 +104,7 @@ struct IgemmArgs {
   int M, JH, JW;              // rows = N*JH*JW
   int ist_h, ist_w;
   int pad_mode;
+  int dil;                    // > 1: A is read on a grid dilated by dil (zeros between real pixels; halo kernel only)
   int vec_ok;                 // A rows 16-byte aligned: vector loads allowed
   const void* Wp;             // packed weights [Npad][nunits*16]
   int Nout;                   // real n'
@@ -310,6 +311,7 @@ struct HaloArgs {
   int pad_mode, vec_ok;        // vec_ok: 16-byte loads of whole chunks stay inside each pixel row
   int N, JH, JW, tiles_h, tiles_w;
   int TH, TW, IMG, SH, SW;    // sub-tile shape, sub-tiles per block, A-grid stride of the taps
+  int dil;                    // > 1: halo coordinates are on A dilated by dil (zero between real pixels)
   int hcap;                   // halo pixels per LDS buffer (>= IMG*HH*HW)
   int ksplit, kps;            // split over k-steps (grid.z); > 1 -> fp32 partials into ws
   float* ws;                  // [ksplit][N*JH*JW][Nout] partial slices (class-local rows)
