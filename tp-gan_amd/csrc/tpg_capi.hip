@@ -185,10 +185,11 @@ static std::vector<Prob> subpixel_probs(int OH, int OW, int kh, int kw, int sh, 
   return v;
 }
 
-// stride 2 on maps of <= 32 x 32 outputs (A/B hooks TPG_NO_DILATED, TPG_DILATED_MAXPIX)
+// stride 2 on maps of <= 64 x 64 outputs (A/B hooks TPG_NO_DILATED, TPG_DILATED_MAXPIX; 64x64: conv2
+// s2 dgrad 0.096 -> 0.039 ms, step -0.3 ms)
 static bool use_dilated(int OH, int OW, int kh, int kw, int sh, int sw, int pad_mode) {
   static const bool off = getenv("TPG_NO_DILATED") != nullptr;
-  static const int maxpix = getenv("TPG_DILATED_MAXPIX") ? atoi(getenv("TPG_DILATED_MAXPIX")) : 32 * 32;
+  static const int maxpix = getenv("TPG_DILATED_MAXPIX") ? atoi(getenv("TPG_DILATED_MAXPIX")) : 64 * 64;
   return !off && sh == 2 && sw == 2 && pad_mode == TPG_PAD_ZERO && kh <= 5 && kw <= 5 && OH * OW <= maxpix;
 }
 
