@@ -47,6 +47,9 @@ SHAPES = {
     "local_up": (32, 512, 5, 5, 256, 3, 2, 1, True, 1, ACT_RELU, False),
     "up_16": (32, 576, 8, 8, 512, 3, 2, 1, True, 1, ACT_RELU, False),
     "up_64": (32, 416, 32, 32, 128, 3, 2, 1, True, 1, ACT_RELU, False),
+    "first_7x7": (32, 3, 128, 128, 64, 7, 1, 3, False, 0, ACT_LEAKY, False),
+    "dec_img": (32, 32, 128, 128, 3, 3, 1, 1, False, 0, ACT_NONE, False),
+    "d_first": (64, 3, 128, 128, 64, 3, 2, 1, False, 0, ACT_LEAKY, False),
     "up_32": (32, 768, 16, 16, 256, 3, 2, 1, True, 1, ACT_RELU, False),
 }
 

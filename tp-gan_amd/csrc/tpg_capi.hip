@@ -274,7 +274,8 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   // unit-stride grids, and stride 2 in both directions (halo (2·th + k − 2) x (2·tw + k − 2))
   const int S = a.ist_h;
   static const bool no_s2 = getenv("TPG_HALO_NO_S2") != nullptr;  // (A/B hook)
-  if (a.ntaps < 1 || a.C < 1 || a.ist_h != a.ist_w || (S != 1 && (S != 2 || no_s2))) return;
+  static const int min_c = getenv("TPG_HALO_MINC") ? atoi(getenv("TPG_HALO_MINC")) : 1;  // (A/B hook)
+  if (a.ntaps < 1 || a.C < min_c || a.ist_h != a.ist_w || (S != 1 && (S != 2 || no_s2))) return;
   int dymin = 127, dymax = -128, dxmin = 127, dxmax = -128;
   for (int t = 0; t < a.ntaps; ++t) {
     dymin = std::min<int>(dymin, a.dy[t]); dymax = std::max<int>(dymax, a.dy[t]);
