@@ -269,10 +269,20 @@ __device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bn
   const int64_t base = (int64_t)tr * p.w_sr + (int64_t)ts * p.w_ss +
                        (p.nmode == 0 ? (int64_t)np * p.w_sa : (int64_t)np * p.w_sb);
   const int64_t cstride = p.cmode == 0 ? p.w_sa : p.w_sb;
+  const float* src = p.W + base + (int64_t)c0 * cstride;
+  if (cstride == 1 && row_ok && c0 + EPC <= p.Creal && ((uintptr_t)src % 16) == 0) {
+    // contiguous input channels (the forward images of channels-last weights): 16-byte loads
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int c = c0 + e;
-    o.e[e] = (E)((row_ok && c < p.Creal) ? p.W[base + (int64_t)c * cstride] : 0.f);
+    for (int q = 0; q < EPC / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      o.e[4 * q] = (E)v.x; o.e[4 * q + 1] = (E)v.y; o.e[4 * q + 2] = (E)v.z; o.e[4 * q + 3] = (E)v.w;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const int c = c0 + e;
+      o.e[e] = (E)((row_ok && c < p.Creal) ? p.W[base + (int64_t)c * cstride] : 0.f);
+    }
   }
   reinterpret_cast<uint4*>(p.Wp)[idx] = o.u;
 }
