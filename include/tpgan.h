@@ -97,8 +97,12 @@ typedef struct tpg_conv_desc {
                                      tpg_pack_run produced for this descriptor and op */
 } tpg_conv_desc;
 
-enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2 };  /* CONCURRENT: the op runs beside other
-                                  streams' work (plan grids for a quarter of the chip: fewer splits) */
+enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2, TPG_FLAG_DX_ACCUM = 4 };
+/* CONCURRENT: the op runs beside other streams' work (plan grids for a quarter of the chip:
+   fewer splits).  DX_ACCUM (tpg_conv2d_bwd_data / tpg_conv2d_bwd): dx holds another gradient
+   contribution of the same input on entry and the input-gradient launch adds it in its
+   epilogue (dx = dgrad + dx; e.g. a residual block's shortcut gradient), instead of a
+   separate add; zero-padded, non-GEMM-form geometries only (-32 otherwise). */
 
 /* Workspace bytes needed by op (TPG_OP_*) for this descriptor. */
 size_t tpg_conv2d_workspace(const tpg_conv_desc* d, int32_t op);

@@ -71,7 +71,7 @@ class _FusedSequential(nn.Sequential):
             return pad, mods[0], (mods[1] if len(mods) == 2 else None)
         return None
 
-    def forward(self, x, residual=None, res_scale=1.0, post_act=None):
+    def forward(self, x, residual=None, res_scale=1.0, post_act=None, link_res=None, link_dx=None):
         parts = self._parts()
         if parts is not None:
             pad, layer, act = parts
@@ -79,7 +79,7 @@ class _FusedSequential(nn.Sequential):
                 if act is not None:
                     raise RuntimeError("residual fusion expects a conv without activation")
                 act = post_act
-            return _apply_conv(layer, x, pad, act, residual, res_scale)
+            return _apply_conv(layer, x, pad, act, residual, res_scale, link_res, link_dx)
         if residual is not None:
             raise RuntimeError("residual fusion needs a [pad] conv [act] sequence")
         return _generic_forward(self, x)
@@ -104,11 +104,20 @@ def _conv_geom_args(layer, pad_mod):
     return dict(stride=stride, pad=(ph, ph, pw, pw), pad_mode=PAD_ZERO)
 
 
-def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0):
+def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None):
     if tuple(layer.dilation) != (1, 1) or layer.groups != 1:
         raise NotImplementedError("dilated / grouped convolution")
     return tpgan_ops.conv2d(x, layer.weight, layer.bias, act=act, residual=residual, res_scale=res_scale,
-                            **_conv_geom_args(layer, pad_mod))
+                            link_res=link_res, link_dx=link_dx, **_conv_geom_args(layer, pad_mod))
+
+
+def _link_ok(seq):
+    """seq is a fused [conv] [act] whose input gradient can take a parked gradient (GradLink)."""
+    parts = seq._parts() if isinstance(seq, _FusedSequential) else None
+    if parts is None or parts[0] is not None or not isinstance(parts[1], nn.Conv2d):
+        return False
+    layer = parts[1]
+    return layer.padding_mode == "zeros" and layer.kernel_size[0] * layer.kernel_size[1] <= 49
 
 
 def _generic_forward(seq, x):
@@ -265,11 +274,17 @@ class ResidualBlock(nn.Module):
     def forward(self, x):
         short = self.shortcut(x) if len(self.shortcut._modules) else x
         h = x
-        for m in list(self.layers)[:-1]:
-            h = m(h)
+        layers = list(self.layers)
         last = self.layers[-1]
-        if tpgan_ops.act_code(self.activation) is not None and last._parts() is not None:
-            return last(h, residual=short, res_scale=self.scaling_factor, post_act=self.activation)
+        fused_last = tpgan_ops.act_code(self.activation) is not None and last._parts() is not None
+        # identity shortcut: the shortcut gradient is added inside the first conv's input-
+        # gradient launch instead of by autograd (tpgan_ops.GradLink)
+        link = (tpgan_ops.GradLink() if tpgan_ops.RES_LINK["enabled"] and fused_last and short is x and len(layers) >= 2 and _link_ok(layers[0])
+                and torch.is_grad_enabled() else None)
+        for i, m in enumerate(layers[:-1]):
+            h = m(h, link_dx=link) if (i == 0 and link is not None) else m(h)
+        if fused_last:
+            return last(h, residual=short, res_scale=self.scaling_factor, post_act=self.activation, link_res=link)
         lm = list(last._modules.values())
         if (tpgan_ops.act_code(self.activation) is not None and len(lm) == 2 and isinstance(lm[0], nn.Conv2d) and
                 isinstance(lm[1], nn.BatchNorm2d) and not lm[1].training):

@@ -791,9 +791,13 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
   tpg_tensor none;
   memset(&none, 0, sizeof(none));
   const bool refl = !comp && !d->transposed && d->pad_mode == TPG_PAD_REFLECT;
+  // DX_ACCUM: dx's entry values ride in as the epilogue's residual (read, then overwritten by
+  // the same thread): dx = dgrad + dx
+  const bool acc = d->flags & TPG_FLAG_DX_ACCUM;
+  if (acc && (comp || refl)) return fail(-32, "dx accumulation: zero-padded, non-GEMM-form geometries only");
   if (!refl)
-    return run_probs(v, d->dtype, g, w, nullptr, 0, none, 0.f, dx, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws),
-                     ws_bytes, s, pk);
+    return run_probs(v, d->dtype, g, w, nullptr, 0, acc ? dx : none, acc ? 1.f : 0.f, dx, TPG_ACT_NONE, 0.f,
+                     reinterpret_cast<char*>(ws), ws_bytes, s, pk);
   // reflect: gradient of the padded input into a dense NHWC temp, then fold onto dx
   const size_t tmpb = reflect_tmp_bytes(d);
   if (ws_bytes < tmpb) return fail(-20, "workspace too small");
@@ -1058,6 +1062,9 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   if (!g_is_gy && (rc = check_tensor(g, d->dtype, "g"))) return rc;
   const tpg_tensor& G = g_is_gy ? gy : g;
   bool have_g = g_is_gy, bias_done = false, dx_done = false;
+  const bool acc = dx.data && (d->flags & TPG_FLAG_DX_ACCUM);
+  if (acc && (bwd_data_composite(d, nullptr, nullptr) || (!d->transposed && d->pad_mode == TPG_PAD_REFLECT)))
+    return fail(-32, "dx accumulation: zero-padded, non-GEMM-form geometries only");
   // pre-packed weights that the input-gradient plan of these tensors cannot use: report it
   // (-21) before anything is launched, so the caller's retry with fp32 weights adds nothing twice
   if ((d->flags & TPG_FLAG_WPACKED) && dx.data &&
@@ -1081,8 +1088,9 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
       mk.M = y; mk.G = g; mk.act = d->act; mk.slope = d->slope;
       tpg_tensor none;
       memset(&none, 0, sizeof(none));
-      rc = run_probs(v, d->dtype, gy, w, nullptr, 0, none, 0.f, dx, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws),
-                     ws_bytes, s, packed ? reinterpret_cast<const char*>(w.data) : nullptr, &mk);
+      rc = run_probs(v, d->dtype, gy, w, nullptr, 0, acc ? dx : none, acc ? 1.f : 0.f, dx, TPG_ACT_NONE, 0.f,
+                     reinterpret_cast<char*>(ws), ws_bytes, s, packed ? reinterpret_cast<const char*>(w.data) : nullptr,
+                     &mk);
       if (rc == 0) have_g = dx_done = true;
       else if (rc != -31) return rc;
     }

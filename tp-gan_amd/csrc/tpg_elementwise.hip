@@ -268,6 +268,58 @@ __global__ __launch_bounds__(256) void copy4d_kernel(int N, int C, int H, int W,
   }
 }
 
+// Pixel-group copy: one thread per (pixel, 8 consecutive channels), offsets computed once
+// per thread (not per element).  Any input layout (NCHW images read coalesced along w) into
+// a channels-last output; 16-byte loads / stores where both rows hold the whole group at
+// 16-byte alignment and the dtypes are 16-bit.  (Concats into channel slices, to_cl.)
+__global__ __launch_bounds__(256) void copy4d_grp_kernel(int N, int C, int H, int W, int G, tpg_tensor in,
+                                                         tpg_tensor out, int vin, int vout) {
+  const int total = N * H * W * G;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int gi = idx % G;
+  const int pix = idx / G;
+  const int w = pix % W, t = pix / W;
+  const int h = t % H, n = t / H;
+  const int c0 = gi * 8;
+  const int nc = min(8, C - c0);
+  const int64_t io = n * in.stride[0] + (int64_t)c0 * in.stride[1] + h * in.stride[2] + w * in.stride[3];
+  const int64_t oo = n * out.stride[0] + (int64_t)c0 * out.stride[1] + h * out.stride[2] + w * out.stride[3];
+  float v[8];
+  if (vin && nc == 8) {
+    const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(in.data) + io);
+    const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint16_t b = (uint16_t)(q[e >> 1] >> (16 * (e & 1)));
+      v[e] = in.dtype == TPG_BF16 ? __uint_as_float((uint32_t)b << 16) : (float)__builtin_bit_cast(_Float16, b);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = e < nc ? ld_any(in.data, in.dtype, io + e * in.stride[1]) : 0.f;
+  }
+  if (vout && nc == 8) {
+    uint32_t q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t lo, hi;
+      if (out.dtype == TPG_BF16) {
+        lo = __builtin_bit_cast(uint16_t, (__bf16)v[2 * e]);
+        hi = __builtin_bit_cast(uint16_t, (__bf16)v[2 * e + 1]);
+      } else {
+        lo = __builtin_bit_cast(uint16_t, (_Float16)v[2 * e]);
+        hi = __builtin_bit_cast(uint16_t, (_Float16)v[2 * e + 1]);
+      }
+      q[e] = (uint32_t)lo | ((uint32_t)hi << 16);
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out.data) + oo) = uint4{q[0], q[1], q[2], q[3]};
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e < nc) st_any(out.data, out.dtype, oo + e * out.stride[1], v[e]);
+  }
+}
+
 // ------------------------------------------------------------------ LocalFuser --
 struct FuseGeom {
   tpg_tensor part[4];
@@ -522,7 +574,19 @@ extern "C" int32_t tpg_colsum_impl(int32_t n, int32_t c, int32_t h, int32_t w, t
 
 extern "C" int32_t tpg_copy4d_impl(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor in, tpg_tensor out,
                                     hipStream_t s) {
-  hipLaunchKernelGGL(copy4d_kernel, dim3(grid_for((int64_t)n * c * h * w)), dim3(256), 0, s, n, c, h, w, in, out);
+  const int G = (c + 7) / 8;
+  if ((int64_t)n * h * w * G < (1ll << 31) - 256) {
+    // 16-byte groups: 16-bit dtype, channel stride 1, every group start 16-byte aligned
+    auto vec = [&](const tpg_tensor& t) {
+      return (t.dtype == TPG_BF16 || t.dtype == TPG_F16) && t.stride[1] == 1 && t.stride[0] % 8 == 0 &&
+             t.stride[2] % 8 == 0 && t.stride[3] % 8 == 0 && ((uintptr_t)t.data & 15) == 0;
+    };
+    const int total = n * h * w * G;
+    hipLaunchKernelGGL(copy4d_grp_kernel, dim3((total + 255) / 256), dim3(256), 0, s, n, c, h, w, G, in, out,
+                       (int)vec(in), (int)vec(out));
+  } else {
+    hipLaunchKernelGGL(copy4d_kernel, dim3(grid_for((int64_t)n * c * h * w)), dim3(256), 0, s, n, c, h, w, in, out);
+  }
   return (int)hipGetLastError();
 }
 

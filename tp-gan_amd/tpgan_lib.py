@@ -38,6 +38,7 @@ class ConvDesc(ctypes.Structure):
 
 FLAG_WPACKED = 1
 FLAG_CONCURRENT = 2
+FLAG_DX_ACCUM = 4
 
 
 EXPORTS = {

@@ -17,7 +17,7 @@ import os
 
 import torch
 
-from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_DX_ACCUM, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
                        PAD_REFLECT,
                        PAD_ZERO, TPG_BF16, TPG_F32, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load,
                        stream_ptr, tt)
@@ -388,7 +388,7 @@ class _ConvAct(torch.autograd.Function):
     saved input and output, never the pre-activation)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam):
+    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res=None, link_dx=None):
         lib = load()
         dtype = get_compute_dtype()
         ctx.in_dtype = x.dtype
@@ -428,14 +428,19 @@ class _ConvAct(torch.autograd.Function):
         ctx.bparam = bias
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.x_dtype = x.dtype
+        ctx.link_res, ctx.link_dx = link_res, link_dx
         return y
 
     @staticmethod
     def backward(ctx, gy):
         if torch.is_grad_enabled():  # create_graph=True (WGAN-GP): differentiable backward
-            return _conv_act_backward_graph(ctx, gy)
+            return tuple(_conv_act_backward_graph(ctx, gy)) + (None, None)
         if FUSED_BWD["enabled"]:
-            return _conv_act_backward_fused(ctx, gy)
+            return _conv_act_backward_fused(ctx, gy) + (None, None)
+        return _ConvAct._backward_three_calls(ctx, gy) + (None, None)
+
+    @staticmethod
+    def _backward_three_calls(ctx, gy):
         lib = load()
         x, weight, y = ctx.saved_tensors
         d = ctx.d
@@ -524,7 +529,16 @@ def _conv_act_backward_fused(ctx, gy):
     if need_db:
         fused_b = _fused_target(ctx.bparam) is not None
         dbias = ctx.bparam.grad if fused_b else torch.zeros(cout, dtype=torch.float32, device=y.device)
-    dx = new_act(*x.shape, dtype=dtype, device=x.device) if need_dx else None
+    # a residual block's parked shortcut gradient (GradLink): accumulated by the dgrad launch
+    acc = None
+    if ctx.link_dx is not None and ctx.link_dx.g is not None:
+        acc, ctx.link_dx.g = ctx.link_dx.g, None
+    if need_dx and acc is not None and tuple(acc.shape) == tuple(x.shape) and acc.dtype == dtype:
+        dx = acc  # dgrad is added into the parked buffer in place
+        acc = None
+        d.flags = d.flags | FLAG_DX_ACCUM
+    else:
+        dx = new_act(*x.shape, dtype=dtype, device=x.device) if need_dx else None
     dw = dwv = None
     if need_dw:
         tgt = _fused_target(ctx.wparam)
@@ -559,6 +573,9 @@ def _conv_act_backward_fused(ctx, gy):
         lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), tt(wv), tt(y), tt(gy), tt(g), tt(fx), tt(dwt), bptr,
                                    wsp, wsn, stream_ptr()), d, pk)
     _probe_end(e0, d, "bwd", _conv_flops(d) * (int(bool(need_dx)) + int(bool(need_dw and not tune_first))))
+    d.flags = d.flags & ~FLAG_DX_ACCUM
+    if acc is not None and dx is not None:  # (not accumulated in the launch: shape / dtype mismatch)
+        dx = dx + acc
     if tune_first:
         algo, ks = _tuned_wgrad(lib, d, x, g, dwv)
         d.algo, d.ksplit = algo, ks
@@ -577,7 +594,11 @@ def _conv_act_backward_fused(ctx, gy):
     dres = None
     if ctx.has_res and ctx.needs_input_grad[3]:
         dres = g if ctx.res_scale == 1.0 else g * ctx.res_scale
-        if dres.dtype != ctx.res_dtype:
+        if ctx.link_res is not None and dres is not gy and dres.dtype == dtype:
+            # park it for the block's first conv (its input-gradient launch adds it)
+            ctx.link_res.g = dres
+            dres = None
+        elif dres.dtype != ctx.res_dtype:
             dres = dres.to(ctx.res_dtype)
     return dx, dw, dbias, dres, None, None, None, None, None
 
@@ -732,14 +753,40 @@ def _fused_target(p):
 
 
 def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_ZERO, act=None, residual=None,
-           res_scale=1.0, transposed=False, output_padding=(0, 0), wparam=None):
-    """Functional entry: act is an activation module (LeakyReLU / ReLU) or None."""
+           res_scale=1.0, transposed=False, output_padding=(0, 0), wparam=None, link_res=None, link_dx=None):
+    """Functional entry: act is an activation module (LeakyReLU / ReLU) or None.  link_res /
+    link_dx: a GradLink shared by a residual block's last conv (residual = the block input)
+    and its first conv (input = the block input), see GradLink."""
     code = act_code(act)
     if code is None:
         raise ValueError("activation %r cannot be fused" % (act,))
     kh, kw = weight.shape[2], weight.shape[3]
     geom = ConvGeom(kh, kw, stride, pad, pad_mode, transposed, output_padding)
-    return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale), wparam)
+    return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale), wparam, link_res,
+                          link_dx)
+
+
+RES_LINK = {"enabled": not os.environ.get("TPG_NO_RES_LINK")}  # (A/B, tests: off = autograd sums it)
+
+
+class GradLink(object):
+    """Hand-off of a residual block's shortcut gradient (ModificationLayer.ResidualBlock,
+    reference ModificationLayer.py:233-302).  The block input x feeds both the first conv and,
+    as the residual, the last one, so autograd would sum two gradients of x with a separate
+    add.  Instead the last conv's fused backward parks its residual gradient here (returning
+    None for it) and the first conv's input-gradient launch adds it in its epilogue
+    (TPG_FLAG_DX_ACCUM: dx = dgrad + parked gradient, written into the parked buffer).  The
+    first conv's backward always runs after the last conv's (it needs its output gradient);
+    the double-backward and three-call paths leave the link unused."""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+    @staticmethod
+    def accepts(geom):
+        """Geometries whose input-gradient launch can accumulate (zero padding, no GEMM form)."""
+        return geom.pad_mode == PAD_ZERO and not geom.transposed and geom.kh * geom.kw <= 49
 
 
 def linear(x, weight, bias=None, act=None, image_hw=None):
