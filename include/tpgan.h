@@ -16,6 +16,7 @@
  *   tpg_conv2d_bwd_filter   the weight gradient (accumulated into fp32)
  *   tpg_act_bwd             activation' mask (LeakyReLU 0.01 / ReLU, from the saved output)
  *                           + bias gradient
+ *   tpg_fold_taps           im2col-lite for the 3-channel convs (taps folded into channels)
  *   tpg_copy4d              dtype/layout conversion and torch.cat into a channel slice
  *                           (D_and_G_model.py:100,102,104,293,298,307,311,312,317,318,323,324)
  *   tpg_local_fuse_fwd/bwd  LocalFuser (D_and_G_model.py:132-159): zero-pad + max over 4 parts
@@ -161,6 +162,15 @@ int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, flo
  * (an out view offset into a wider channels-last buffer implements torch.cat). */
 int32_t tpg_copy4d(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor in, tpg_tensor out,
                    tpg_stream_t stream);
+
+/* Tap folding for thin-input convs (3-channel images): y[n][(fy*fw + fx)*c + ci][y'][x'] =
+ * x[n][ci][y'*sh + fy - pt][x'*sw + fx - pl] (zero outside), y logical [n, fh*fw*c, oh, ow];
+ * the conv on y with the weight viewed as [out][fh*fw*c][kh/fh][kw/fw] equals the original
+ * (ModificationLayer.py:54-123 conv() on the RGB inputs of D_and_G_model.py:33,193,415).
+ * backward != 0: x (as dx) = the sum over every folded copy of y (as the incoming gradient). */
+int32_t tpg_fold_taps(int32_t n, int32_t c, int32_t h, int32_t w, int32_t fh, int32_t fw, int32_t sh, int32_t sw,
+                      int32_t pt, int32_t pl, int32_t oh, int32_t ow, tpg_tensor x, tpg_tensor y, int32_t backward,
+                      tpg_stream_t stream);
 
 /* LocalFuser: part k (logical [n, c, ph[k], pw[k]]) is placed at (top[k], left[k]) of an
  * out_h x out_w zero canvas; y = max over k, argmax = first k attaining it (uint8, NHWC order). */

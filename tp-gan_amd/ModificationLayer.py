@@ -107,6 +107,13 @@ def _conv_geom_args(layer, pad_mod):
 def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None):
     if tuple(layer.dilation) != (1, 1) or layer.groups != 1:
         raise NotImplementedError("dilated / grouped convolution")
+    if (isinstance(layer, nn.Conv2d) and layer.in_channels <= 4 and residual is None and link_dx is None and
+            pad_mod is None and layer.padding_mode == "zeros" and layer.kernel_size != (1, 1)):
+        # thin input: taps folded into channels (tpgan_ops.conv2d_folded)
+        ph, pw = layer.padding
+        y = tpgan_ops.conv2d_folded(x, layer.weight, layer.bias, tuple(layer.stride), (ph, ph, pw, pw), act)
+        if y is not None:
+            return y
     return tpgan_ops.conv2d(x, layer.weight, layer.bias, act=act, residual=residual, res_scale=res_scale,
                             link_res=link_res, link_dx=link_dx, **_conv_geom_args(layer, pad_mod))
 

@@ -24,6 +24,8 @@
 extern "C" int32_t tpg_act_bwd_impl(int32_t, int32_t, int32_t, int32_t, int32_t, float, tpg_tensor, tpg_tensor,
                                      tpg_tensor, float*, hipStream_t);
 extern "C" int32_t tpg_copy4d_impl(int32_t, int32_t, int32_t, int32_t, tpg_tensor, tpg_tensor, hipStream_t);
+extern "C" int32_t tpg_fold_taps_impl(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
+                                      int32_t, int32_t, int32_t, tpg_tensor, tpg_tensor, int32_t, hipStream_t);
 extern "C" int32_t tpg_fuse_fwd_impl(int32_t, int32_t, int32_t, int32_t, const tpg_tensor*, const int32_t*,
                                       const int32_t*, const int32_t*, const int32_t*, tpg_tensor, uint8_t*, hipStream_t);
 extern "C" int32_t tpg_fuse_bwd_impl(int32_t, int32_t, int32_t, int32_t, tpg_tensor, const uint8_t*, const tpg_tensor*,
@@ -1095,13 +1097,16 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
       else if (rc != -31) return rc;
     }
   }
-  // 2. otherwise the activation backward pass materialises g (and sums the bias)
+  // 2. otherwise the activation backward pass materialises g (and sums the bias when there is
+  // no weight gradient: with one, the weight-gradient launch sums it, the same order whether
+  // the caller runs the weight gradient here or as a second call on another stream)
   if (!have_g) {
-    rc = hip_check(tpg_act_bwd_impl(d->n, d->out_c, d->out_h, d->out_w, d->act, d->slope, gy, y, g, dbias, s),
+    float* db = dw.data ? nullptr : dbias;
+    rc = hip_check(tpg_act_bwd_impl(d->n, d->out_c, d->out_h, d->out_w, d->act, d->slope, gy, y, g, db, s),
                    "act_bwd");
     if (rc) return rc;
     have_g = true;
-    bias_done = dbias != nullptr;
+    bias_done = db != nullptr;
   }
   if (dx.data && !dx_done) {
     if ((rc = tpg_conv2d_bwd_data(d, G, w, dx, ws, ws_bytes, stream))) return rc;
@@ -1128,6 +1133,17 @@ extern "C" int32_t tpg_copy4d(int32_t n, int32_t c, int32_t h, int32_t w, tpg_te
   if (!in.data || !out.data) return fail(-10, "copy4d: NULL tensor");
   if ((int64_t)n * c * h * w == 0) return 0;
   return hip_check(tpg_copy4d_impl(n, c, h, w, in, out, (hipStream_t)stream), "copy4d");
+}
+
+extern "C" int32_t tpg_fold_taps(int32_t n, int32_t c, int32_t h, int32_t w, int32_t fh, int32_t fw, int32_t sh,
+                                 int32_t sw, int32_t pt, int32_t pl, int32_t oh, int32_t ow, tpg_tensor x, tpg_tensor y,
+                                 int32_t backward, tpg_stream_t stream) {
+  if (!x.data || !y.data) return fail(-10, "fold_taps: NULL tensor");
+  if (fh < 1 || fw < 1 || sh < 1 || sw < 1 || n < 0 || c < 1 || (int64_t)fh * fw * c > 4096)
+    return fail(-2, "fold_taps: bad geometry");
+  if ((int64_t)n * (backward ? (int64_t)h * w * c : (int64_t)oh * ow * fh * fw * c) == 0) return 0;
+  return hip_check(tpg_fold_taps_impl(n, c, h, w, fh, fw, sh, sw, pt, pl, oh, ow, x, y, backward, (hipStream_t)stream),
+                   "fold_taps");
 }
 
 extern "C" int32_t tpg_local_fuse_fwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, const tpg_tensor* parts,

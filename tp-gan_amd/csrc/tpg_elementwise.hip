@@ -320,6 +320,73 @@ __global__ __launch_bounds__(256) void copy4d_grp_kernel(int N, int C, int H, in
   }
 }
 
+// ------------------------------------------------------------------ tap folding --
+// Thin-input convs (3-channel images): the taps of an FH x FW window are folded into the
+// channel dimension, y[n][y'][x'][(fy*FW + fx)*C + c] = x[n][y'*sh + fy - pt][x'*sw + fx - pl][c]
+// (zero outside), so the conv that follows reads 16-27 live channels per 32-channel MFMA
+// k-step instead of 3 (the weights are a strided view of the same memory).  One thread per
+// output (pixel, folded channel); the backward gathers dx from every folded copy.
+__global__ __launch_bounds__(256) void fold_taps_kernel(int N, int C, int H, int W, int FH, int FW, int sh, int sw,
+                                                        int pt, int pl, int OH, int OW, tpg_tensor x, tpg_tensor y) {
+  const int CF = FH * FW * C;
+  const int64_t total = (int64_t)N * OH * OW * CF;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int cf = (int)(idx % CF);
+    const int64_t pix = idx / CF;
+    const int ox = (int)(pix % OW);
+    const int64_t t = pix / OW;
+    const int oy = (int)(t % OH), n = (int)(t / OH);
+    const int tap = cf / C, c = cf - tap * C;
+    const int iy = oy * sh + tap / FW - pt, ix = ox * sw + tap % FW - pl;
+    float v = 0.f;
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      v = ld_any(x.data, x.dtype, n * x.stride[0] + c * x.stride[1] + iy * x.stride[2] + ix * x.stride[3]);
+    st_any(y.data, y.dtype, n * y.stride[0] + cf * y.stride[1] + oy * y.stride[2] + ox * y.stride[3], v);
+  }
+}
+
+__global__ __launch_bounds__(256) void unfold_taps_kernel(int N, int C, int H, int W, int FH, int FW, int sh, int sw,
+                                                          int pt, int pl, int OH, int OW, tpg_tensor gy, tpg_tensor dx) {
+  const int64_t total = (int64_t)N * H * W * C;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const int64_t pix = idx / C;
+    const int ix = (int)(pix % W);
+    const int64_t t = pix / W;
+    const int iy = (int)(t % H), n = (int)(t / H);
+    float acc = 0.f;
+    for (int fy = 0; fy < FH; ++fy) {
+      const int ny = iy + pt - fy;
+      if (ny < 0 || ny % sh) continue;
+      const int oy = ny / sh;
+      if (oy >= OH) continue;
+      for (int fx = 0; fx < FW; ++fx) {
+        const int nx = ix + pl - fx;
+        if (nx < 0 || nx % sw) continue;
+        const int ox = nx / sw;
+        if (ox >= OW) continue;
+        const int cf = (fy * FW + fx) * C + c;
+        acc += ld_any(gy.data, gy.dtype, n * gy.stride[0] + cf * gy.stride[1] + oy * gy.stride[2] + ox * gy.stride[3]);
+      }
+    }
+    st_any(dx.data, dx.dtype, n * dx.stride[0] + c * dx.stride[1] + iy * dx.stride[2] + ix * dx.stride[3], acc);
+  }
+}
+
+extern "C" int32_t tpg_fold_taps_impl(int32_t n, int32_t c, int32_t h, int32_t w, int32_t fh, int32_t fw, int32_t sh,
+                                      int32_t sw, int32_t pt, int32_t pl, int32_t oh, int32_t ow, tpg_tensor x,
+                                      tpg_tensor y, int32_t backward, hipStream_t s) {
+  if (backward)
+    hipLaunchKernelGGL(unfold_taps_kernel, dim3(grid_for((int64_t)n * h * w * c)), dim3(256), 0, s, n, c, h, w, fh, fw,
+                       sh, sw, pt, pl, oh, ow, y, x);
+  else
+    hipLaunchKernelGGL(fold_taps_kernel, dim3(grid_for((int64_t)n * oh * ow * fh * fw * c)), dim3(256), 0, s, n, c, h,
+                       w, fh, fw, sh, sw, pt, pl, oh, ow, x, y);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------ LocalFuser --
 struct FuseGeom {
   tpg_tensor part[4];

@@ -55,6 +55,7 @@ EXPORTS = {
     "tpg_act_bwd": (ctypes.c_int32, [ctypes.c_int32] * 5 + [ctypes.c_float, TpgTensor, TpgTensor, TpgTensor,
                                                              ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_copy4d": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor, ctypes.c_void_p]),
+    "tpg_fold_taps": (ctypes.c_int32, [ctypes.c_int32] * 12 + [TpgTensor, TpgTensor, ctypes.c_int32, ctypes.c_void_p]),
     "tpg_local_fuse_fwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [ctypes.POINTER(TpgTensor)] +
                            [ctypes.POINTER(ctypes.c_int32)] * 4 + [TpgTensor, ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_local_fuse_bwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, ctypes.c_void_p,

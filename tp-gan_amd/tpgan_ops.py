@@ -113,6 +113,27 @@ def concurrent(on=True):
         _CONCURRENT.pop()
 _SIDE = {}
 
+# Weight gradients on a side stream (wgrad_side_stream()): inside the block, a fused conv
+# backward launches its input gradient (and g) on the current stream and its weight / bias
+# gradient on a per-device side stream behind an event, so the next layer's input gradient
+# overlaps this layer's weight gradient; leaving the block joins the side stream.
+WGRAD_SIDE = {"stream": None, "enabled": os.environ.get("TPG_WGRAD_SIDE", "1") != "0"}
+
+
+@contextlib.contextmanager
+def wgrad_side_stream(device=None, on=True):
+    if not (on and WGRAD_SIDE["enabled"] and torch.cuda.is_available()):
+        yield
+        return
+    st = side_streams(device if device is not None else torch.cuda.current_device(), 1)[0]
+    prev = WGRAD_SIDE["stream"]
+    WGRAD_SIDE["stream"] = st
+    try:
+        yield
+    finally:
+        WGRAD_SIDE["stream"] = prev
+        torch.cuda.current_stream().wait_stream(st)
+
 
 def side_streams(device, n):
     """n persistent side HIP streams of `device` (created once)."""
@@ -480,7 +501,7 @@ class _ConvAct(torch.autograd.Function):
             tgt = _fused_target(ctx.wparam)
             if tgt is not None:  # dW accumulates straight into the flat gradient buffer
                 dw = None
-                dwv = tgt if tgt.shape == weight.shape else tgt.view(weight.shape)
+                dwv = _grad_view(tgt, weight, ctx.wparam)
             else:
                 dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
                 if weight.dim() == 4 and weight.is_contiguous(memory_format=torch.channels_last):
@@ -543,7 +564,7 @@ def _conv_act_backward_fused(ctx, gy):
     if need_dw:
         tgt = _fused_target(ctx.wparam)
         if tgt is not None:  # dW accumulates straight into the flat gradient buffer
-            dwv = tgt if tgt.shape == weight.shape else tgt.view(weight.shape)
+            dwv = _grad_view(tgt, weight, ctx.wparam)
         else:
             dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
             if weight.dim() == 4 and weight.is_contiguous(memory_format=torch.channels_last):
@@ -566,14 +587,40 @@ def _conv_act_backward_fused(ctx, gy):
     fx = _fix_c1(dx) if dx is not None else None
     dwt = dwv if (need_dw and not tune_first) else None
     bptr = dbias.data_ptr() if dbias is not None else None
+    # weight / bias gradient on the side stream (only into the flat buffers: nothing autograd
+    # would accumulate on this stream); not while capturing a graph or probing
+    side = WGRAD_SIDE["stream"]
+    # (a residual block's last conv parks its g for the first conv's in-place dgrad, GradLink:
+    # its weight gradient stays on this stream, ahead of that write)
+    split = (side is not None and dwt is not None and dw is None and (dbias is None or fused_b) and
+             ctx.link_res is None and PROBE["match"] is None and not torch.cuda.is_current_stream_capturing())
     e0 = _probe_begin(d, "bwd")
     _run_maybe_packed(
-        lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk), tt(y), tt(gy), tt(g), tt(fx), tt(dwt), bptr,
-                                   wsp, wsn, stream_ptr()),
-        lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), tt(wv), tt(y), tt(gy), tt(g), tt(fx), tt(dwt), bptr,
-                                   wsp, wsn, stream_ptr()), d, pk)
+        lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk), tt(y), tt(gy), tt(g), tt(fx),
+                                   tt(None if split else dwt), None if split else bptr, wsp, wsn, stream_ptr()),
+        lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), tt(wv), tt(y), tt(gy), tt(g), tt(fx),
+                                   tt(None if split else dwt), None if split else bptr, wsp, wsn, stream_ptr()), d, pk)
     _probe_end(e0, d, "bwd", _conv_flops(d) * (int(bool(need_dx)) + int(bool(need_dw and not tune_first))))
     d.flags = d.flags & ~FLAG_DX_ACCUM
+    if split:
+        gt = gy if g_is_gy else g  # (g now holds act'(y) * gy: the second call takes it as is)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        side.wait_event(ev)
+        d2 = _plain_desc(d)
+        d2.algo, d2.ksplit = d.algo, d.ksplit
+        with torch.cuda.stream(side):
+            check(lib.tpg_conv2d_bwd(ctypes.byref(d2), tt(x), tt(None), tt(None), tt(gt), tt(gt), tt(None), tt(dwt),
+                                     bptr, None, 0, stream_ptr()))
+            if fused_b:
+                _grad_ready(ctx.bparam)
+            _grad_ready(ctx.wparam)
+        for t in (x, gt):  # (their memory stays reserved until the side stream has read it)
+            t.record_stream(side)
+        fused_b = False
+        dbias = None  # (accumulated into the flat buffer on the side stream)
+        dw = None
+        need_dw = False
     if acc is not None and dx is not None:  # (not accumulated in the launch: shape / dtype mismatch)
         dx = dx + acc
     if tune_first:
@@ -739,6 +786,15 @@ def _grad_ready(p):
         h(p)
 
 
+def _grad_view(tgt, weight, wparam):
+    """The flat-gradient view matching `weight`, a view (reshape / tap-folded as_strided) of
+    the parameter wparam: FlatParams lays p.grad out exactly like p.data."""
+    if tgt.shape == weight.shape and tgt.stride() == weight.stride():
+        return tgt
+    return tgt.as_strided(weight.shape, weight.stride(),
+                          tgt.storage_offset() + weight.storage_offset() - wparam.storage_offset())
+
+
 def _fused_target(p):
     """p.grad when p opted into in-place gradient accumulation (FlatParams sets
     p._tpg_fused_grad): the HIP kernels then add into the flat fp32 gradient buffer
@@ -769,6 +825,74 @@ def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_Z
 RES_LINK = {"enabled": not os.environ.get("TPG_NO_RES_LINK")}  # (A/B, tests: off = autograd sums it)
 
 
+class _FoldTaps(torch.autograd.Function):
+    """tpg_fold_taps: an FH x FW tap window folded into channels (see conv2d_folded)."""
+
+    @staticmethod
+    def forward(ctx, x, fh, fw, sh, sw, pt, pl, oh, ow):
+        lib = load()
+        dtype = get_compute_dtype()
+        n, c, h, w = x.shape
+        y = new_act(n, fh * fw * c, oh, ow, dtype, x.device)
+        check(lib.tpg_fold_taps(n, c, h, w, fh, fw, sh, sw, pt, pl, oh, ow, tt(x), tt(y), 0, stream_ptr()))
+        ctx.geo = (n, c, h, w, fh, fw, sh, sw, pt, pl, oh, ow)
+        ctx.x_dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        # (differentiable under create_graph, WGAN-GP: the unfold's own backward is the fold)
+        return (_UnfoldTaps.apply(gy, ctx.geo, ctx.x_dtype),) + (None,) * 8
+
+
+class _UnfoldTaps(torch.autograd.Function):
+    """The fold's backward: dx = the sum over every folded copy (linear; its backward is the fold)."""
+
+    @staticmethod
+    def forward(ctx, gy, geo, x_dtype):
+        n, c, h, w, fh, fw, sh, sw, pt, pl, oh, ow = geo
+        ctx.geo = geo
+        dx = new_act(n, c, h, w, x_dtype, gy.device)
+        check(load().tpg_fold_taps(n, c, h, w, fh, fw, sh, sw, pt, pl, oh, ow, tt(dx), tt(gy), 1, stream_ptr()))
+        return dx
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, h, w, fh, fw, sh, sw, pt, pl, oh, ow = ctx.geo
+        return _FoldTaps.apply(g, fh, fw, sh, sw, pt, pl, oh, ow), None, None
+
+
+FOLD = {"enabled": os.environ.get("TPG_NO_FOLD") is None}
+
+
+def conv2d_folded(x, weight, bias, stride, pad, act):
+    """A zero-padded Conv2d on a thin input (the 3-channel images; reference
+    ModificationLayer.py:54-123 conv() at D_and_G_model.py:33,193,415) as a conv over the
+    tap-folded input: all KHxKW taps folded (KH*KW*C <= 32: one 32-channel MFMA k-step, a 1x1
+    conv) or, at stride 1, the KW horizontal taps (a KHx1 conv on KW*C channels) -- instead
+    of KH*KW k-steps with 3 live channels of 32.  The weight is a strided view of the same
+    channels-last memory ([co][ky][kx][c] is also [co][(ky*KW+kx)*C+c]), so its gradient
+    accumulates in place.  Returns None when the shape is not covered."""
+    if not FOLD["enabled"] or not x.is_cuda or weight.dim() != 4:
+        return None
+    co, c, kh, kw = weight.shape
+    if weight.stride() != (kh * kw * c, 1, kw * c, c):  # (channels-last weights only)
+        return None
+    n, _, h, w = x.shape
+    sh, sw = stride
+    pt, pb, pl, pr = pad
+    oh, ow = (h + pt + pb - kh) // sh + 1, (w + pl + pr - kw) // sw + 1
+    if kh * kw * c <= 32:
+        xf = _FoldTaps.apply(x, kh, kw, sh, sw, pt, pl, oh, ow)
+        wf = weight.as_strided((co, kh * kw * c, 1, 1), (kh * kw * c, 1, kh * kw * c, kh * kw * c))
+        return conv2d(xf, wf, bias, act=act, wparam=weight)
+    if sh == 1 and sw == 1 and kw * c <= 32:
+        xf = _FoldTaps.apply(x, 1, kw, 1, 1, 0, pl, h, ow)
+        wf = weight.as_strided((co, kw * c, kh, 1), (kh * kw * c, 1, kw * c, kw * c))
+        return conv2d(xf, wf, bias, pad=(pt, pb, 0, 0), act=act, wparam=weight)
+    return None
+
+
 class GradLink(object):
     """Hand-off of a residual block's shortcut gradient (ModificationLayer.ResidualBlock,
     reference ModificationLayer.py:233-302).  The block input x feeds both the first conv and,
@@ -789,11 +913,39 @@ class GradLink(object):
         return geom.pad_mode == PAD_ZERO and not geom.transposed and geom.kh * geom.kw <= 49
 
 
+class _FlattenNCHW(torch.autograd.Function):
+    """[B, C, H, W] channels-last map -> [B, C*H*W, 1, 1] in NCHW flattening order (the
+    reference's view(B, -1) before fc1, D_and_G_model.py:289); the backward hands the
+    gradient back channels-last."""
+
+    @staticmethod
+    def forward(ctx, x):
+        b, c, h, w = x.shape
+        ctx.shape = (b, c, h, w)
+        return x.contiguous().view(b, c * h * w, 1, 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        b, c, h, w = ctx.shape
+        return to_cl(g.reshape(b, c, h, w), g.dtype)
+
+
+# fc1 (a Linear on an NCHW-flattened map): as a 1x1 conv on the flattened activation instead
+# of an HxW full-kernel conv on the channels-last map, so its weight gradient walks the weight
+# in its own (NCHW) order -- coalesced rows instead of 4-byte accesses 256 B apart (the
+# full-kernel form's weight-gradient launch took 0.34 ms for 67 MB)
+LINEAR_FLAT = {"enabled": os.environ.get("TPG_LINEAR_FULLKERNEL", "0") == "0"}
+
+
 def linear(x, weight, bias=None, act=None, image_hw=None):
     """nn.Linear on [B, K] (or a [B, C, H, W] map flattened in NCHW order, fc1 at
-    D_and_G_model.py:289) as a full-kernel conv; returns [B, out]."""
+    D_and_G_model.py:289); returns [B, out]."""
     out_f, in_f = weight.shape
-    if x.dim() == 4:
+    if x.dim() == 4 and LINEAR_FLAT["enabled"] and x.is_cuda:
+        b = x.shape[0]
+        xf = _FlattenNCHW.apply(to_cl(x, get_compute_dtype()))
+        y = conv2d(xf, weight.view(out_f, in_f, 1, 1), bias, act=act, wparam=weight)
+    elif x.dim() == 4:
         b, c, h, w = x.shape
         w4 = weight.view(out_f, c, h, w)
         y = conv2d(x, w4, bias, act=act, wparam=weight)

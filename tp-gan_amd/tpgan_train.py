@@ -20,6 +20,8 @@ Parameters of G and D live in one flat fp32 buffer each (params are views), so t
 optimizer is one HIP Adam launch per network and the data-parallel exchange is one
 RCCL all-reduce per network (torch.distributed, backend "nccl" = RCCL over xGMI).
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -394,7 +396,8 @@ class TPGANTrainer:
                 loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
             if self.dsync is not None and not self._capturing:
                 self.dsync.begin()
-            (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
+            with tpgan_ops.wgrad_side_stream():  # (weight gradients overlap the next input gradients)
+                (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
 
     def gradient_penalty(self, real, fake, alpha=None):
@@ -421,20 +424,11 @@ class TPGANTrainer:
             set_requires_grad(D.parameters(), False)
             d_gen = D(fake).float()
             set_requires_grad(D.parameters(), True)
-        f32 = fake.float()
         front = b["frontal"]
-        l_pix = w["weight_128"] * (f32 - front).abs().mean()
-        l_local = ((le_f.float() - b["frontal_left_eye"]).abs().mean() +
-                   (re_f.float() - b["frontal_right_eye"]).abs().mean() +
-                   (no_f.float() - b["frontal_nose"]).abs().mean() +
-                   (mo_f.float() - b["frontal_mouth"]).abs().mean()) / 4.0
-        l_sym = (f32 - f32.flip(3)).abs().mean()
-        l_adv = -d_gen.mean()
-        l_tv = total_variation(f32)
-        l_ce = F.cross_entropy(pred.float(), b["label"])
-        loss_G = (w["weight_pixelwise"] * l_pix + w["weight_pixelwise_local"] * l_local +
-                  w["weight_symmetry"] * l_sym + w["weight_adv_G"] * l_adv + w["weight_total_varation"] * l_tv +
-                  w["weight_cross_entropy"] * l_ce)
+        args = (fake, le_f, re_f, no_f, mo_f, d_gen, pred, front, b["frontal_left_eye"], b["frontal_right_eye"],
+                b["frontal_nose"], b["frontal_mouth"], b["label"])
+        loss_G = self._g_losses(*args)
+        f32 = fake.float() if self.identity_fn is not None else None
         if self.identity_fn is not None:
             if self._id_pre is not None:
                 l_ip = self.identity_fn(f32, front, pre=self._id_pre)
@@ -444,8 +438,25 @@ class TPGANTrainer:
             loss_G = loss_G + w["weight_identity_preserving"] * l_ip
         if self.gsync is not None and not self._capturing:
             self.gsync.begin()
-        (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
+        with tpgan_ops.wgrad_side_stream():
+            (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
         self._st["loss_G"] = loss_G.detach()
+
+    def _g_losses(self, fake, le_f, re_f, no_f, mo_f, d_gen, pred, front, fle, fre, fno, fmo, label):
+        """The G-step's pixel, local, symmetry, adversarial, total-variation and identity-class
+        losses (build-defined, config.py:59-82 weights)."""
+        w = self.w
+        f32 = fake.float()
+        l_pix = w["weight_128"] * (f32 - front).abs().mean()
+        l_local = ((le_f.float() - fle).abs().mean() + (re_f.float() - fre).abs().mean() +
+                   (no_f.float() - fno).abs().mean() + (mo_f.float() - fmo).abs().mean()) / 4.0
+        l_sym = (f32 - f32.flip(3)).abs().mean()
+        l_adv = -d_gen.mean()
+        l_tv = total_variation(f32)
+        l_ce = F.cross_entropy(pred.float(), label)
+        return (w["weight_pixelwise"] * l_pix + w["weight_pixelwise_local"] * l_local +
+                w["weight_symmetry"] * l_sym + w["weight_adv_G"] * l_adv + w["weight_total_varation"] * l_tv +
+                w["weight_cross_entropy"] * l_ce)
 
     def _phase_c(self, b):
         self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale)
