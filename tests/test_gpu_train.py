@@ -294,8 +294,8 @@ def test_deterministic_mode_bit_identical(gpu):
 
 
 def test_wgrad_side_stream_bit_identical(gpu):
-    """Weight gradients on the side stream (tpgan_ops.wgrad_side_stream, the train step's
-    default) against all of them on the launching stream: deterministic mode, bf16, from the
+    """Weight gradients on the side stream (tpgan_ops.wgrad_side_stream, TPG_WGRAD_SIDE=1)
+    against all of them on the launching stream: deterministic mode, bf16, from the
     same state -- parameters, gradients and Adam moments bit-identical (a side-stream read of
     a buffer the main stream already overwrote, or a missing join, would show here)."""
     import tpgan_ops
@@ -316,7 +316,7 @@ def test_wgrad_side_stream_bit_identical(gpu):
                 tr.step(b)
                 torch.cuda.synchronize()
             finally:
-                tpgan_ops.WGRAD_SIDE["enabled"] = True
+                tpgan_ops.WGRAD_SIDE["enabled"] = False
             res.setdefault(on, []).append(
                 [t.clone() for t in (tr.fG.data, tr.fD.data, tr.fG.grad, tr.fD.grad, tr.fG.exp_avg_sq)])
     for a, c in zip(res[True][0], res[False][0]):

@@ -117,7 +117,10 @@ _SIDE = {}
 # backward launches its input gradient (and g) on the current stream and its weight / bias
 # gradient on a per-device side stream behind an event, so the next layer's input gradient
 # overlaps this layer's weight gradient; leaving the block joins the side stream.
-WGRAD_SIDE = {"stream": None, "enabled": os.environ.get("TPG_WGRAD_SIDE", "1") != "0"}
+# (off by default: measured 37.86 / 37.97 ms/step with it vs 37.80 without -- the overlap
+# it buys is paid back in host time per layer (event, wait, record_stream), and the host
+# already spends ~31.6 ms enqueueing a ~38 ms step; TPG_WGRAD_SIDE=1 turns it on)
+WGRAD_SIDE = {"stream": None, "enabled": os.environ.get("TPG_WGRAD_SIDE", "0") != "0"}
 
 
 @contextlib.contextmanager
@@ -396,10 +399,17 @@ def _run_maybe_packed(fn_packed, fn_plain, d, pk):
     check(fn_plain())
 
 
+_WS_BYTES = {}  # (op, descriptor) -> workspace bytes: the C planner runs once per shape, not per call
+
+
 def _ws(lib, desc, op, device):
-    nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
-    if nb == 0:
-        check(-1)
+    key = (op, desc.flags, desc.algo, desc.ksplit, lib.tpg_get_deterministic()) + _desc_tuple(desc)
+    nb = _WS_BYTES.get(key)
+    if nb is None:
+        nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
+        if nb == 0:
+            check(-1)
+        _WS_BYTES[key] = nb
     return torch.empty(nb, dtype=torch.uint8, device=device)
 
 
