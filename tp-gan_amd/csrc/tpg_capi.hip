@@ -567,7 +567,8 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
   if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
   const bool vA = vec_ok(A, dtype);
   if (mk) {  // the mask mode has no generic-kernel fallback: decide before launching anything
-    if (v.size() != 1 || !v[0].halo || v[0].h.ntaps < 2 || (v[0].h.var & 2) || !vA) return -31;
+    // (the 512-row and stride-2 halo configs, ids >= 24, have no masked variant)
+    if (v.size() != 1 || !v[0].halo || v[0].hcfg >= 24 || v[0].h.ntaps < 2 || (v[0].h.var & 2) || !vA) return -31;
     const int64_t ext = (int64_t)(v[0].h.N - 1) * std::abs(A.stride[0]) + (int64_t)(v[0].h.A_H - 1) * std::abs(A.stride[2]) +
                         (int64_t)(v[0].h.A_W - 1) * std::abs(A.stride[3]) + v[0].h.C + 64;
     const int64_t extm = (int64_t)(v[0].h.N - 1) * mk->M.stride[0] + (int64_t)(v[0].h.A_H - 1) * mk->M.stride[2] +
@@ -1073,10 +1074,10 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
       (!vec_ok(G, d->dtype) || bwd_data_composite(d, &G, &dx) != bwd_data_composite(d, nullptr, nullptr)))
     return fail(-21, "pre-packed weights assume the halo kernel / dense NHWC; these tensors need another plan");
   // 1. the input gradient with the activation' applied while its halo is staged (writes g)
-  // (maps up to 64 x 64: there the separate activation-backward pass is latency-bound and the
-  // fusion wins; on the 128 x 128 layers it streams at ~5 TB/s and the masked staging costs as
-  // much as it saves (measured: 42.1 ms/step at 4096, 42.5 with every map, 43.0 with none))
-  static const int64_t mask_maxpix = getenv("TPG_MASK_MAXPIX") ? atoll(getenv("TPG_MASK_MAXPIX")) : 64 * 64;
+  // (round 1 measured 42.1 ms/step with maps up to 64 x 64, 42.5 with every map, 43.0 with
+  // none; after the 512-row and stride-2 tiles -- which have no masked variant and now fall
+  // back to the separate pass -- every map measured 37.39 vs 37.54 / 37.56 at 64 x 64)
+  static const int64_t mask_maxpix = getenv("TPG_MASK_MAXPIX") ? atoll(getenv("TPG_MASK_MAXPIX")) : 1 << 30;
   if (!have_g && dx.data && !d->transposed && d->stride_h == 1 && d->stride_w == 1 && d->pad_mode == TPG_PAD_ZERO &&
       (int64_t)d->out_h * d->out_w <= mask_maxpix &&
       d->in_h == d->out_h && d->in_w == d->out_w && gy.dtype == d->dtype && y.dtype == d->dtype &&
