@@ -14,4 +14,5 @@ for ab in "$@"; do
 done
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench2.log 2>&1
 timeout -k 10 200 python -u tools/cpu_overhead.py > $O/cpu_overhead.log 2>&1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 echo done

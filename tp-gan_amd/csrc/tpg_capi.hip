@@ -1102,7 +1102,9 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   // no weight gradient: with one, the weight-gradient launch sums it, the same order whether
   // the caller runs the weight gradient here or as a second call on another stream)
   if (!have_g) {
-    float* db = dw.data ? nullptr : dbias;
+    // (ConvTranspose2d: its weight-gradient kernels never take the bias -- it would cost a
+    // separate column-sum launch, so this pass keeps it)
+    float* db = (dw.data && !d->transposed) ? nullptr : dbias;
     rc = hip_check(tpg_act_bwd_impl(d->n, d->out_c, d->out_h, d->out_w, d->act, d->slope, gy, y, g, db, s),
                    "act_bwd");
     if (rc) return rc;

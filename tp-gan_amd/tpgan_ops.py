@@ -601,9 +601,11 @@ def _conv_act_backward_fused(ctx, gy):
     # would accumulate on this stream); not while capturing a graph or probing
     side = WGRAD_SIDE["stream"]
     # (a residual block's last conv parks its g for the first conv's in-place dgrad, GradLink:
-    # its weight gradient stays on this stream, ahead of that write)
+    # its weight gradient stays on this stream, ahead of that write; a ConvTranspose2d sums its
+    # bias in the activation-backward pass, so it stays unsplit too)
     split = (side is not None and dwt is not None and dw is None and (dbias is None or fused_b) and
-             ctx.link_res is None and PROBE["match"] is None and not torch.cuda.is_current_stream_capturing())
+             ctx.link_res is None and not ctx.geom.transposed and PROBE["match"] is None and
+             not torch.cuda.is_current_stream_capturing())
     e0 = _probe_begin(d, "bwd")
     _run_maybe_packed(
         lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk), tt(y), tt(gy), tt(g), tt(fx),
