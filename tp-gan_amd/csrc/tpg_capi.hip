@@ -51,7 +51,11 @@ static int g_det = 0;  // tpg_set_deterministic
 static thread_local int g_share = 1;
 struct ShareScope {
   int prev;
-  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share) { g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? 4 : 1; }
+  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share) {
+    // share of the chip a concurrent op plans for (1 / share); TPG_CONCURRENT_SHARE: A/B hook
+    static const int share = getenv("TPG_CONCURRENT_SHARE") ? std::max(1, atoi(getenv("TPG_CONCURRENT_SHARE"))) : 4;
+    g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? share : 1;
+  }
   ~ShareScope() { g_share = prev; }
 };
 
