@@ -44,7 +44,9 @@ def parse():
     ap.add_argument("--img-size", type=int, default=None)
     ap.add_argument("--dtype", choices=["bf16", "fp16", "fp32"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: OMP_NUM_THREADS, i.e. this process's CPU share -- 16 "
+                         "on the GPU box, whose os.cpu_count() reports the whole host -- else os.cpu_count())")
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--graph", action="store_true",
@@ -101,10 +103,12 @@ def main():
 
     # warm-up (autotunes the weight-gradient tiles), one eager step counted for the
     # algorithmic FLOPs, then the step is captured as hipGraph(s)
+    # (next_b: the next step's batch -- here the same resident one -- so that, data-parallel,
+    # its D(real) pass runs under the G all-reduce tail)
     for _ in range(max(args.warmup - 1, 0)):
-        trainer.step(batch)
+        trainer.step(batch, next_b=batch)
     tpgan_ops.reset_flops()
-    trainer.step(batch)
+    trainer.step(batch, next_b=batch)
     flops_step = sum(tpgan_ops.FLOPS.values())
     if os.environ.get("TPG_TUNE_DUMP") and rank == 0:  # the weight-gradient tiles the autotuner picked
         tpgan_ops.save_tuning(os.environ["TPG_TUNE_DUMP"])
@@ -116,7 +120,7 @@ def main():
         run = trainer.step_graphed
     else:
         def run():
-            return trainer.step(batch)
+            return trainer.step(batch, next_b=batch)
 
     if not graphed:
         tpgan_ops.PROBE["match"] = match
@@ -124,9 +128,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step HIP events on the launching stream (every step ends on it: side streams join)
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    marks[0].record()
+    for i in range(args.steps):
         run()
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -137,6 +145,9 @@ def main():
     elapsed = float(elapsed.item())
     ms_per_step = elapsed / args.steps * 1e3
     faces = world * B * args.steps / elapsed
+    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
+    step_med = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1] +
+                                                                          step_ms[len(step_ms) // 2])
 
     # dominant-kernel probe: HIP events around each launch on its launch stream.  Graph
     # nodes cannot be bracketed, so with graphs the probe runs eager steps right after the
@@ -166,9 +177,10 @@ def main():
         from oracle.cpu_step import time_cpu_step
         cb = min(B, args.cpu_batch) if args.img_size == 128 else 0
         if cb:
-            r = time_cpu_step(B=cb, iters=args.cpu_iters, threads=args.cpu_threads)
-            cpu = {"value": round(r["full_fps"], 4), "unit": "faces/s", "cores": r["threads"], "kind": "port",
-                   "cpu_model": r["cpu"],
+            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count()
+            r = time_cpu_step(B=cb, iters=args.cpu_iters, threads=threads)
+            cpu = {"value": round(r["full_fps"], 4), "unit": "faces/s", "cores": r["threads"], "threads": r["threads"],
+                   "host_cpu_count": os.cpu_count(), "kind": "port", "cpu_model": r["cpu"],
                    "sample": "oracle/cpu_step.py full G+D train step incl. both Adam updates, 128x128, B=%d, fp32 "
                              "aten CPU, 1 warm-up + median of %d steps (%.2f s/step)" % (cb, args.cpu_iters,
                                                                                         r["full_s"]),
@@ -209,6 +221,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step_median": round(step_med, 3),
+        "step_ms_events": {"min": round(step_ms[0], 3), "median": round(step_med, 3), "max": round(step_ms[-1], 3),
+                           "n": len(step_ms), "source": "HIP events between consecutive steps on the launch stream"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -195,6 +195,11 @@ int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg,
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  float grad_scale, float* state, tpg_stream_t stream);
 
+/* Overflow guard of the loss-scaled fp16 step (torch.cuda.amp.GradScaler's skip): state[3] :=
+ * 1 if any of grad[0..numel) is inf / NaN, else 0 (device-side, graph-capturable).  A tpg_adam
+ * call on the same state then leaves parameters, moments and the step counter untouched. */
+int32_t tpg_grad_check(int64_t numel, const float* grad, float* state, tpg_stream_t stream);
+
 /* ---- identity-feature extractors (MobileNetV2.py, ResNet.py, FeatureExtract.py) ---- */
 
 /* Depthwise Conv2d (groups == in_c == out_c, MobileNetV2.py:105), kernels up to 3x3, zero

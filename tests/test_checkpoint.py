@@ -181,3 +181,32 @@ def test_checkpoint_hparam_mismatch(tmp_path):
     assert tr3.load_checkpoint(str(tmp_path), 1, adopt_hparams=True) == 1
     assert tr3.betas == (0.9, 0.999) and tr3.lr == 3e-4
     assert torch.equal(tr3.fG.data, tr.fG.data)
+
+
+def test_checkpoint_mismatch_leaves_trainer_untouched(tmp_path):
+    """a hyperparameter mismatch found in D's file (G's is fine) used to raise after
+    G had been restored and D's Adam moments overwritten.  Every file is now checked first, so
+    the failed load leaves weights, moments and step counts of both networks as they were."""
+    tr = _tiny_trainer(0)
+    tr.save_checkpoint(str(tmp_path), 4)
+    p = os.path.join(str(tmp_path), "D", "optimizer_epoch_4.pth")
+    ck = torch.load(p, weights_only=True)
+    ck["optimizer"]["param_groups"][0]["betas"] = (0.9, 0.999)
+    torch.save(ck, p)
+    tr2 = _tiny_trainer(1)
+    before = [t.clone() for f in (tr2.fG, tr2.fD) for t in (f.data, f.exp_avg, f.exp_avg_sq, f.adam_state)]
+    with pytest.raises(ValueError, match="D/4"):
+        tr2.load_checkpoint(str(tmp_path), 4)
+    after = [t for f in (tr2.fG, tr2.fD) for t in (f.data, f.exp_avg, f.exp_avg_sq, f.adam_state)]
+    for a, b in zip(before, after):
+        assert torch.equal(a, b)
+    # and a shape mismatch in a model file is caught the same way, before anything moves
+    ck = torch.load(p, weights_only=True)
+    ck["optimizer"]["param_groups"][0]["betas"] = (0.5, 0.999)
+    key = next(iter(ck["model"]))
+    ck["model"][key] = torch.zeros(1)
+    torch.save(ck, p)
+    with pytest.raises(ValueError, match="shape"):
+        tr2.load_checkpoint(str(tmp_path), 4)
+    for a, b in zip(before, after):
+        assert torch.equal(a, b)

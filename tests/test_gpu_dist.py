@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, gp=False):
     sys.path[:0] = [REPO, os.path.join(REPO, "tp-gan_amd")]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -36,47 +36,55 @@ def _worker(rank, world, port, q):
         torch.manual_seed(10 + rank)  # different init per rank: the broadcast must unify it
         G = DG.Generator(64, 347, use_batchnorm=False).to(dev)
         D = DG.Discriminator().to(dev)
-        tr = tpgan_train.TPGANTrainer(G, D, compute_dtype=torch.bfloat16, bucket_mb=16.0)
+        tr = tpgan_train.TPGANTrainer(G, D, compute_dtype=torch.bfloat16, bucket_mb=16.0, gradient_penalty=gp)
         b = tpgan_train.synthetic_batch(2, dev, seed=100 + rank)
-        issued_early, d_early = [], []
+        issued_early, d_early, ahead = [], [], []
 
-        def wrap(sync, out):
+        def wrap(sync, out, ra=None):
             orig = sync.finish
 
             def finish():
                 out.append(sync.next)  # buckets already issued when the backward returned
+                if ra is not None:
+                    # G's tail: when the main stream is about to wait for the last G buckets,
+                    # the next step's D(real) pass must already be enqueued ahead of that wait
+                    ra.append(tr._d_real_next is not None)
                 return orig()
             sync.finish = finish
 
-        wrap(tr.gsync, issued_early)
+        wrap(tr.gsync, issued_early, ahead)
         wrap(tr.dsync, d_early)
         for _ in range(3):
-            tr.step(b)
+            tr.step(b, next_b=b)  # (D(real) of the next step under the G all-reduce tail)
         torch.cuda.synchronize()
         sums = torch.stack([tr.fG.data.double().sum(), tr.fD.data.double().sum(),
                             tr.fG.data.double().square().sum()]).cpu()
         q.put((rank, sums.tolist(), issued_early, len(tr.gsync.buckets), list(tr.fG.offsets[:50]),
-               tr.gsync.order_learned, d_early, len(tr.dsync.buckets), tr.dsync.order_learned))
+               tr.gsync.order_learned, d_early, len(tr.dsync.buckets), tr.dsync.order_learned, ahead))
     except Exception as e:
-        q.put((rank, repr(e), [], 0, [], False, [], 0, False))
+        q.put((rank, repr(e), [], 0, [], False, [], 0, False, []))
         raise
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_dp_overlap_two_ranks_one_gpu(gpu):
+@pytest.mark.parametrize("gp", [False, True])
+def test_dp_overlap_two_ranks_one_gpu(gpu, gp):
+    """gp: WGAN-GP, whose double backward adds a second gradient contribution to D's
+    parameters -- D's buckets then wait for the contribution count learned on step 1 and go
+    out during the backward from step 2 on."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, gp)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=280) for _ in range(world)])
     for p in procs:
         p.join(60)
-    (r0, s0, e0, nb0, off0, l0, de0, dnb0, dl0), (r1, s1, e1, nb1, off1, l1, de1, dnb1, dl1) = res
+    (r0, s0, e0, nb0, off0, l0, de0, dnb0, dl0, a0), (r1, s1, e1, nb1, off1, l1, de1, dnb1, dl1, a1) = res
     assert isinstance(s0, list) and isinstance(s1, list), (s0, s1)
     assert s0 == s1  # identical replicas after 3 steps
     assert nb0 == nb1 and nb0 > 10 and l0 and l1
@@ -85,6 +93,8 @@ def test_dp_overlap_two_ranks_one_gpu(gpu):
     # D: bucketed during the D-step backward as well
     assert dnb0 == dnb1 and dnb0 > 3 and dl0 and dl1
     assert max(de0) > 0 and max(de1) > 0
+    # every step's G-bucket tail had the next D(real) pass enqueued before it
+    assert a0 == [True] * 3 and a1 == [True] * 3, (a0, a1)
 
 
 LR_EQ = 1e-4  # the bench's learning rate
@@ -138,18 +148,27 @@ def _equiv_worker(rank, world, port, q):
             load_det(D, "D/", torch.float32)
             return G.to(dev), D.to(dev)
 
-        def snap(tr, G, D, loss, scale):
+        def snap(tr, G, D, loss, scale, gD=None):
             return ([p.grad.detach().clone() / scale for p in G.parameters()],
+                    [g / scale for g in gD] if gD is not None else
                     [p.grad.detach().clone() / scale for p in D.parameters()],
                     [p.detach().clone() for p in G.parameters()],
                     [p.detach().clone() for p in D.parameters()], loss, _moments(tr))
 
         full = [tpgan_train.synthetic_batch(4, dev, seed=300 + s) for s in range(2)]
+        halves = [{k: v[2 * rank:2 * rank + 2] for k, v in b.items()} for b in full]
         res, ref, got = {}, [], []
         with tpgan_ops.deterministic():
             G2, D2 = models()
             t2 = tpgan_train.TPGANTrainer(G2, D2, lr=LR_EQ, compute_dtype=torch.float32, use_dropout=False,
                                           bucket_mb=16.0)
+            # D's step gradient, read before the D(real) pass of the next batch re-zeroes fD.grad
+            orig_ra = t2._real_ahead
+
+            def real_ahead(nb):
+                t2._gD_step = [p.grad.detach().clone() for p in D2.parameters()]
+                return orig_ra(nb)
+            t2._real_ahead = real_ahead
             if rank == 0:
                 G1, D1 = models()
                 t1 = tpgan_train.TPGANTrainer(G1, D1, lr=LR_EQ, compute_dtype=torch.float32, use_dropout=False,
@@ -160,20 +179,24 @@ def _equiv_worker(rank, world, port, q):
                         _copy_state(t1, t2)
                     out = t1.step(b)
                     torch.cuda.synchronize()
-                    ref.append(snap(t1, G1, D1, float(out["loss_G"]), 1))
+                    ref.append(snap(t1, G1, D1, (float(out["loss_G"]), float(out["loss_D"])), 1))
                 dist.barrier()
-                half = {k: v[2 * rank:2 * rank + 2] for k, v in b.items()}
-                out = t2.step(half)
+                # the DP run announces its next batch: step 2's D(real) pass runs at the end of
+                # step 1, under the G all-reduce tail (real_ahead)
+                out = t2.step(halves[s], next_b=halves[s + 1] if s + 1 < len(halves) else None)
                 torch.cuda.synchronize()
-                lg = torch.tensor([float(out["loss_G"])], dtype=torch.float64)
-                dist.all_reduce(lg)  # the 1-GPU loss is the mean of the two half-batch means
-                got.append(snap(t2, G2, D2, float(lg) / world, world))
+                if s == 0:
+                    res["real_ahead"] = t2._d_real_next is not None
+                lg = torch.tensor([float(out["loss_G"]), float(out["loss_D"])], dtype=torch.float64)
+                dist.all_reduce(lg)  # the 1-GPU losses are the means of the two half-batch means
+                got.append(snap(t2, G2, D2, (float(lg[0]) / world, float(lg[1]) / world), world, t2._gD_step))
             res["relayout"] = bool(t2.gsync.order_learned)
         if rank == 0:
             cat = lambda ts: torch.cat([t.double().reshape(-1) for t in ts]).cpu()  # noqa: E731
             for s, ((gG, gD, pG, pD, lG, mo1), (hG, hD, qG, qD, mG, mo2)) in enumerate(zip(ref, got)):
                 res["step%d" % s] = {
-                    "loss": abs(lG - mG) / abs(lG),
+                    "loss": abs(lG[0] - mG[0]) / abs(lG[0]),
+                    "lossD": abs(lG[1] - mG[1]) / max(abs(lG[1]), 1e-3),
                     "gradG": rel(cat(hG), cat(gG)), "gradD": rel(cat(hD), cat(gD)),
                     "paramG": rel(cat(qG), cat(pG)), "paramD": rel(cat(qD), cat(pD)),
                     "moments": max(rel(cat(b), cat(a)) for a, b in zip(mo1, mo2))}
@@ -209,12 +232,12 @@ def test_dp_equals_single_gpu_at_global_batch(gpu):
         p.join(60)
     r0 = res[0]
     assert isinstance(r0, dict), r0
-    assert r0["relayout"]
+    assert r0["relayout"] and r0["real_ahead"]
     for s in ("step0", "step1"):
         m = r0[s]
-        assert m["loss"] < 1e-6, (s, m)
+        assert m["loss"] < 1e-6 and m["lossD"] < 1e-5, (s, m)
         assert m["moments"] < 1e-5, (s, m)
-        assert m["gradG"] < 1e-5 and m["gradD"] < 1e-5, (s, m, r0["worstG" + s[-1]])
+        assert m["gradG"] < 1e-5 and m["gradD"] < 1e-5, (s, m)
         # parameters: Adam's first steps normalise every element (g / (|g| + eps)), so an
         # element whose gradient is itself at the 1e-7 floor moves by up to ~lr either way
         assert m["paramG"] < 1e-5 and m["paramD"] < 1e-5, (s, m)

@@ -91,3 +91,33 @@ def test_step_flops_match_survey():
     with torch.no_grad(), FlopCounterMode(display=False) as fc:
         O.discriminator(PD, out[0])
     assert abs(fc.get_total_flops() / 1e9 - 1.298) < 0.01
+
+
+def test_tuning_file_roundtrip_and_old_keys(tmp_path):
+    """weight-gradient tuning files written before the concurrency flag joined the
+    cache key (18-field keys) load as whole-chip (flag 0) entries instead of never matching."""
+    import tpgan_ops
+    from tpgan_lib import FLAG_CONCURRENT, ConvDesc
+    saved = dict(tpgan_ops.AUTOTUNE["cache"])
+    try:
+        d = ConvDesc()
+        d.n, d.in_c, d.in_h, d.in_w, d.out_c, d.out_h, d.out_w, d.kh, d.kw = 32, 64, 40, 40, 64, 40, 40, 3, 3
+        d.stride_h = d.stride_w = 1
+        k0 = tpgan_ops._wgrad_key(d)
+        d.flags = FLAG_CONCURRENT
+        k1 = tpgan_ops._wgrad_key(d)
+        assert len(k0[1]) == len(k1[1]) == tpgan_ops._WGRAD_KEY_LEN and k0 != k1
+        tpgan_ops.AUTOTUNE["cache"].clear()
+        tpgan_ops.AUTOTUNE["cache"][k1] = (7, 4)
+        p = str(tmp_path / "tune.json")
+        tpgan_ops.save_tuning(p)
+        old = str(tmp_path / "old.json")
+        json.dump([[list(k0[1][:-1]), "wgrad", [12, 2]]], open(old, "w"))
+        tpgan_ops.AUTOTUNE["cache"].clear()
+        tpgan_ops.load_tuning(p)
+        tpgan_ops.load_tuning(old)
+        assert tpgan_ops.AUTOTUNE["cache"][k1] == (7, 4)
+        assert tpgan_ops.AUTOTUNE["cache"][k0] == (12, 2)
+    finally:
+        tpgan_ops.AUTOTUNE["cache"].clear()
+        tpgan_ops.AUTOTUNE["cache"].update(saved)

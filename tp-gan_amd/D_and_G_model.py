@@ -273,7 +273,7 @@ class Generator(nn.Module):
             # on the current stream; autograd replays each op's backward on its forward
             # stream, so the backward overlaps the same way.
             main = torch.cuda.current_stream()
-            side = tpgan_ops.side_streams(I128.device, 4)
+            side = tpgan_ops.side_streams(I128.device, 4, "local")
             outs = []
             for st, path, x in zip(side, paths, patches):
                 st.wait_stream(main)

@@ -77,7 +77,8 @@ class IdentityPreservingLoss(nn.Module):
         if not (tpgan_ops.MULTISTREAM and real.is_cuda):
             return None
         main = torch.cuda.current_stream()
-        st = tpgan_ops.side_streams(real.device, 1)[0]
+        # (a stream of its own: the weight-gradient side stream would queue behind this work)
+        st = tpgan_ops.side_streams(real.device, 1, "identity")[0]
         st.wait_stream(main)
         with torch.cuda.stream(st), torch.no_grad(), tpgan_ops.compute_dtype(self.compute_dtype), \
                 tpgan_ops.concurrent():

@@ -1192,6 +1192,15 @@ extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, floa
   return hip_check(rc, "adam");
 }
 
+extern "C" int32_t tpg_grad_check_impl(int64_t, const float*, float*, hipStream_t);
+
+extern "C" int32_t tpg_grad_check(int64_t numel, const float* grad, float* state, tpg_stream_t stream) {
+  if (!grad || !state) return fail(-10, "grad_check: NULL pointer");
+  const int rc = tpg_grad_check_impl(numel, grad, state, (hipStream_t)stream);
+  if (rc == -1) return fail(-15, "grad_check: gradient buffer must be 16-byte aligned");
+  return hip_check(rc, "grad_check");
+}
+
 extern "C" void tpg_set_deterministic(int32_t on) { __atomic_store_n(&g_det, on ? 1 : 0, __ATOMIC_RELAXED); }
 extern "C" int32_t tpg_get_deterministic(void) { return tpg::deterministic(); }
 

@@ -514,7 +514,10 @@ int launch_reflect_fold(int N, int C, int H, int W, int pt, int pb, int pl, int 
 // v = b2 v + (1-b2) g^2; p -= lr / (1-b1^t) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
 // The bias corrections come from a device state {step, 1-b1^t, sqrt(1-b2^t)} that
 // adam_sched_kernel advances, so a captured hipGraph replays correct steps.
+// st[3] != 0 (set by grad_finite_kernel for this step's gradients): the step is skipped --
+// counter, moments and parameters stay as they are (torch.cuda.amp.GradScaler's skip).
 __global__ void adam_sched_kernel(float* st, float b1, float b2, int32_t host_step) {
+  if (st[3] != 0.f) return;
   const float t = host_step > 0 ? (float)host_step : st[0] + 1.f;
   st[0] = t;
   st[1] = 1.f - powf(b1, t);
@@ -533,6 +536,7 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
                                                    float* __restrict__ m, float* __restrict__ v, float lr, float b1,
                                                    float b2, float eps, float wd, const float* __restrict__ st,
                                                    float gscale) {
+  if (st[3] != 0.f) return;  // non-finite gradients this step (grad_finite_kernel)
   const float lr_bc1 = lr / st[1], bc2s = st[2];
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -551,6 +555,20 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
   }
   for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
     adam_one(p[i], gr[i] * gscale, m[i], v[i], lr_bc1, b1, b2, eps, wd, bc2s);
+}
+
+// st[3] := 1 when any gradient element is inf / NaN (st[3] zeroed by a memset node first; every
+// writer stores the same value, so the race is benign).  HBM-bound: 4 B per element.
+__global__ __launch_bounds__(256) void grad_finite_kernel(int64_t n, const float* __restrict__ gr, float* st) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 g = reinterpret_cast<const float4*>(gr)[i];
+    bad |= !(isfinite(g.x) && isfinite(g.y) && isfinite(g.z) && isfinite(g.w));
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) bad |= !isfinite(gr[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) st[3] = 1.f;
 }
 
 }  // namespace tpg
@@ -704,5 +722,16 @@ extern "C" int32_t tpg_adam_impl(int64_t numel, float* param, const float* grad,
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, state,
                      gscale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int32_t tpg_grad_check_impl(int64_t numel, const float* grad, float* state, hipStream_t s) {
+  if (((uintptr_t)grad) % 16) return -1;
+  hipError_t e = hipMemsetAsync(state + 3, 0, sizeof(float), s);
+  if (e) return (int)e;
+  if (numel <= 0) return 0;
+  int blocks = (int)std::min<int64_t>((numel / 4 + 255) / 256, 2048);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(grad_finite_kernel, dim3(blocks), dim3(256), 0, s, numel, grad, state);
   return (int)hipGetLastError();
 }

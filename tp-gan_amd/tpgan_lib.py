@@ -68,6 +68,7 @@ EXPORTS = {
     "tpg_adam": (ctypes.c_int32, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p] + [ctypes.c_float] * 5 + [ctypes.c_int32, ctypes.c_float,
                                                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_grad_check": (ctypes.c_int32, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_dwconv2d_fwd": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, ctypes.c_void_p, TpgTensor,
                                           TpgTensor, ctypes.c_void_p]),
     "tpg_dwconv2d_bwd_data": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), TpgTensor, TpgTensor, TpgTensor,

@@ -128,7 +128,7 @@ def wgrad_side_stream(device=None, on=True):
     if not (on and WGRAD_SIDE["enabled"] and torch.cuda.is_available()):
         yield
         return
-    st = side_streams(device if device is not None else torch.cuda.current_device(), 1)[0]
+    st = side_streams(device if device is not None else torch.cuda.current_device(), 1, "wgrad")[0]
     prev = WGRAD_SIDE["stream"]
     WGRAD_SIDE["stream"] = st
     try:
@@ -138,12 +138,46 @@ def wgrad_side_stream(device=None, on=True):
         torch.cuda.current_stream().wait_stream(st)
 
 
-def side_streams(device, n):
-    """n persistent side HIP streams of `device` (created once)."""
-    key = (torch.device(device).index, n)
+def side_streams(device, n, tag=""):
+    """n persistent side HIP streams of `device` (created once per (n, tag): users that may
+    be in flight at the same time ask with different tags)."""
+    key = (torch.device(device).index, n, tag)
     if key not in _SIDE:
         _SIDE[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
     return _SIDE[key]
+
+
+_ROCTX = [None]
+
+
+def _roctx():
+    if _ROCTX[0] is None:
+        lib = False
+        for name in ("libroctx64.so.4", "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.restype = ctypes.c_int
+                lib.roctxRangePop.restype = ctypes.c_int
+                break
+            except (OSError, AttributeError):
+                lib = False
+        _ROCTX[0] = lib
+    return _ROCTX[0]
+
+
+@contextlib.contextmanager
+def roctx_range(name):
+    """A roctx range (SURVEY.md §5 tracing: G-fwd / D-step / G-step / all-reduce), shown by
+    `rocprofv3 --marker-trace`; a no-op when libroctx64 is absent."""
+    lib = _roctx()
+    if lib:
+        lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        if lib:
+            lib.roctxRangePop()
 
 
 def _ceil8(c):
@@ -249,11 +283,21 @@ def save_tuning(path):
         json.dump([[list(k[1]), k[0], v] for k, v in AUTOTUNE["cache"].items()], f)
 
 
+_WGRAD_KEY_LEN = 19  # _desc_tuple (18 fields) + the concurrency flag
+
+
 def load_tuning(path):
+    """Load a save_tuning file.  Files written before the concurrency flag joined the key
+    (18-field keys) are upgraded: their entries were tuned for the whole chip (flag 0)."""
     import json
     with open(path) as f:
         for key, op, v in json.load(f):
-            AUTOTUNE["cache"][(op, tuple(key))] = tuple(v)  # (tuples of _wgrad_key: shape + concurrency flag)
+            key = tuple(key)
+            if len(key) == _WGRAD_KEY_LEN - 1:
+                key = key + (0,)
+            elif len(key) != _WGRAD_KEY_LEN:
+                raise ValueError("tuning file %s: key of %d fields, expected %d" % (path, len(key), _WGRAD_KEY_LEN))
+            AUTOTUNE["cache"][(op, key)] = tuple(v)
 
 
 def _wgrad_key(d):
@@ -1088,9 +1132,15 @@ def maxout2(x):
     return _Maxout2.apply(x)
 
 
+def grad_check(grad, state):
+    """state[3] := 1 if grad holds an inf / NaN (the next adam_step on `state` then skips)."""
+    check(load().tpg_grad_check(grad.numel(), grad.data_ptr(), state.data_ptr(), stream_ptr()))
+
+
 def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, state, step=0, grad_scale=1.0):
     """In-place Adam on flat fp32 buffers (torch.optim.Adam semantics).  `state` is a device
-    float32[4] {step, bias corrections}; step=0 advances its counter on the device (graph-safe)."""
+    float32[4] {step, bias corrections, skip flag}; step=0 advances its counter on the device
+    (graph-safe); a set skip flag (grad_check) leaves everything untouched."""
     lib = load()
     check(lib.tpg_adam(param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
                        lr, beta1, beta2, eps, weight_decay, int(step), grad_scale, state.data_ptr(), stream_ptr()))

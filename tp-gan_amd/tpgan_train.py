@@ -44,6 +44,7 @@ class FlatParams:
         self.adam_state = torch.zeros(4, dtype=torch.float32, device=device)  # {step, bias corrections}
         self.step = 0
         self.epoch = 0            # bumped by every optimizer update (pre-packed weight images follow it)
+        self.layout_version = 0   # bumped by relayout(): captured hipGraphs hold the old buffers
         self.pack_entries = {}    # tpgan_ops pre-packed weight images of this network's convs
         self.pack_table = None
         self.offsets = []
@@ -71,6 +72,7 @@ class FlatParams:
             off += n
         self.data, self.grad, self.exp_avg, self.exp_avg_sq = new
         self.offsets = offsets
+        self.layout_version += 1
         self.pack_entries = {}  # weights moved: packed images are rebuilt on next use
         self.pack_table = None
         for i, p in enumerate(self.params):
@@ -96,12 +98,21 @@ class FlatParams:
     def zero_grad(self):
         self.grad.zero_()
 
-    def adam(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0):
+    def adam(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0, check_finite=False):
+        """One Adam update of the whole network (one launch).  check_finite (the loss-scaled
+        fp16 step): an inf / NaN anywhere in the gradients skips the update on the device --
+        parameters, moments and the step counter stay as they were (last_step_skipped())."""
         self.step += 1
+        if check_finite:
+            tpgan_ops.grad_check(self.grad, self.adam_state)
         tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
                             weight_decay, self.adam_state, 0, grad_scale)
         self.epoch += 1
         tpgan_ops.repack(self)
+
+    def last_step_skipped(self):
+        """True when the last adam(check_finite=True) found non-finite gradients (synchronises)."""
+        return float(self.adam_state[3]) != 0.0
 
     # ---- checkpoint (SURVEY.md §8f3): torch.optim.Adam's state_dict format, so the files of
     # UtilityMethods.save_optimizer (UtilityMethods.py:78-103) load into either optimizer.
@@ -119,16 +130,34 @@ class FlatParams:
                  "params": list(range(len(self.params)))}
         return {"state": state, "param_groups": [group]}
 
-    def load_optimizer_state_dict(self, sd):
-        """Restore Adam moments and the step count (per parameter, so a checkpoint written
-        before a bucket relayout loads after it).  Missing entries mean zero moments.  Returns
-        the stored hyperparameters {lr, betas, eps, weight_decay} (param_groups[0]); the
-        caller compares them with its own (TPGANTrainer.load_checkpoint)."""
+    def check_optimizer_state_dict(self, sd):
+        """Validate an Adam state_dict against this network without touching any state;
+        returns (step, stored hyperparameters {lr, betas, eps, weight_decay})."""
         st = sd["state"]
         steps = {int(round(float(v["step"]))) for v in st.values()} or {0}
         if len(steps) != 1:
             raise ValueError("optimizer state: parameters at different step counts %s" % sorted(steps))
-        step = steps.pop()
+        for i, v in st.items():
+            if not (0 <= int(i) < len(self.params)):
+                raise ValueError("optimizer state: parameter index %s out of range" % (i,))
+            p = self.params[int(i)]
+            for k in ("exp_avg", "exp_avg_sq"):
+                if tuple(v[k].shape) != tuple(p.shape):
+                    raise ValueError("optimizer state %d/%s: shape %s, parameter %s" %
+                                     (int(i), k, tuple(v[k].shape), tuple(p.shape)))
+        groups = sd.get("param_groups") or [{}]
+        g = groups[0]
+        hp = {k: (tuple(g[k]) if k == "betas" else g[k]) for k in ("lr", "betas", "eps", "weight_decay") if k in g}
+        return steps.pop(), hp
+
+    def load_optimizer_state_dict(self, sd):
+        """Restore Adam moments and the step count (per parameter, so a checkpoint written
+        before a bucket relayout loads after it).  Missing entries mean zero moments.  Returns
+        the stored hyperparameters {lr, betas, eps, weight_decay} (param_groups[0]); the
+        caller compares them with its own (TPGANTrainer.load_checkpoint).  Everything is
+        validated before any state changes."""
+        step, hp = self.check_optimizer_state_dict(sd)
+        st = sd["state"]
         with torch.no_grad():
             self.exp_avg.zero_()
             self.exp_avg_sq.zero_()
@@ -137,17 +166,11 @@ class FlatParams:
                     continue
                 o, n = self.offsets[i], p.numel()
                 for k, buf in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
-                    v = st[i][k]
-                    if tuple(v.shape) != tuple(p.shape):
-                        raise ValueError("optimizer state %d/%s: shape %s, parameter %s" %
-                                         (i, k, tuple(v.shape), tuple(p.shape)))
-                    self._view(buf, p, o, n).copy_(v)
+                    self._view(buf, p, o, n).copy_(st[i][k])
             self.adam_state.zero_()
             self.adam_state[0] = float(step)  # the next launch advances it and recomputes the corrections
         self.step = step
-        groups = sd.get("param_groups") or [{}]
-        g = groups[0]
-        return {k: (tuple(g[k]) if k == "betas" else g[k]) for k in ("lr", "betas", "eps", "weight_decay") if k in g}
+        return hp
 
     def weights_loaded(self):
         """After parameter values were overwritten in place (load_state_dict): rebuild the packed images."""
@@ -196,12 +219,23 @@ class OverlappedGradSync(GradSync):
     their gradients completing (broadcast, so all ranks agree), which turns "bucket k is
     ready" into "the k-th stretch of the backward is done" — DDP's bucket rebuild."""
 
-    def __init__(self, flat, group=None, bucket_mb=32.0):
+    def __init__(self, flat, group=None, bucket_mb=32.0, count_accumulate=False):
         super(OverlappedGradSync, self).__init__(group)
         self.flat = flat
         self.bucket_bytes = int(bucket_mb * 2 ** 20)
         self.active = False
         self.order_learned = False
+        # count_accumulate (WGAN-GP's D): a parameter receives several gradient contributions in
+        # one backward (the fused HIP weight gradient, then autograd's accumulation of the double
+        # backward's); each is counted (the fused path's report, a post-accumulate-grad hook) and
+        # the parameter is ready at the count the first step observed -- that step issues its
+        # buckets only at finish()
+        self.count_accumulate = count_accumulate
+        self.expected = None
+        if count_accumulate:
+            for p in flat.params:
+                if p.requires_grad:
+                    p.register_post_accumulate_grad_hook(self._ready)
         self._build()
 
     def _build(self):
@@ -233,8 +267,13 @@ class OverlappedGradSync(GradSync):
         if self.world == 1:
             return
         self.active = True
-        self.pending = [len(idxs) for idxs in self.buckets]
+        if self.expected is not None:  # parameters that get no gradient at all count as done
+            self.pending = [sum(1 for i in idxs if self.expected[i] > 0) for idxs in self.buckets]
+        else:
+            self.pending = [len(idxs) for idxs in self.buckets]
         self.seen = set()
+        self.counts = [0] * len(self.flat.params)
+        self.last_seq = [-1] * len(self.flat.params)
         self.next = 0
         self.works = []
         self.order = []
@@ -245,16 +284,25 @@ class OverlappedGradSync(GradSync):
         tpgan_ops.GRAD_READY_HOOK[0] = self._ready
 
     def _ready(self, p):
+        if not self.active:
+            return
         i = self.index.get(id(p))
         if i is None or i in self.seen:
             return
-        self.seen.add(i)
-        self.order.append(i)
         b = self.bucket_of[i]
-        if self.flat.grad.is_cuda:
+        if self.flat.grad.is_cuda:  # (one event per contribution: they may come from several streams)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             self.events[b].append(ev)
+        if self.count_accumulate:
+            self.counts[i] += 1
+            if self.expected is None:  # learning step: record, issue nothing before finish()
+                self.last_seq[i] = sum(self.counts)
+                return
+            if self.counts[i] < self.expected[i]:
+                return
+        self.seen.add(i)
+        self.order.append(i)
         self.pending[b] -= 1
         while self.next < len(self.buckets) and self.pending[self.next] == 0:
             self._issue(self.next)
@@ -278,6 +326,12 @@ class OverlappedGradSync(GradSync):
             return
         tpgan_ops.GRAD_READY_HOOK[0] = None
         self.active = False
+        if self.count_accumulate and self.expected is None:
+            # the learning step: contributions per parameter, and the completion order by each
+            # parameter's last contribution (what the buckets will wait for from now on)
+            self.expected = list(self.counts)
+            self.order = sorted((i for i in range(len(self.counts)) if self.counts[i] > 0),
+                                key=lambda i: self.last_seq[i])
         cur = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
         while self.next < len(self.buckets):
             self._issue(self.next, after_stream=cur)
@@ -329,7 +383,7 @@ class TPGANTrainer:
 
     def __init__(self, G, D, lr=1e-4, betas=(0.5, 0.999), compute_dtype=torch.bfloat16, loss_weights=None,
                  gradient_penalty=False, process_group=None, identity_fn=None, use_dropout=True, overlap=True,
-                 bucket_mb=32.0, loss_scale=None):
+                 bucket_mb=32.0, loss_scale=None, real_ahead=None):
         self.G, self.D = G, D
         # fp16 activations / gradients (BASELINE configs[4]): a static loss scale keeps the
         # per-element image gradients (~1/(B*3*H*W)) out of fp16's subnormal range; the scale
@@ -352,11 +406,18 @@ class TPGANTrainer:
         # G's 551 MB of gradients are reduced bucket by bucket during the G backward, D's 54 MB
         # during the D-step backward (buckets of bucket_mb / 4: D's backward is ~5x shorter)
         self.gsync = OverlappedGradSync(self.fG, process_group, bucket_mb) if (overlap and self.world > 1) else None
-        # (not with WGAN-GP: D's parameters then get a second gradient contribution from the
-        # double backward after their first one has been reported ready)
-        self.dsync = (OverlappedGradSync(self.fD, process_group, bucket_mb / 4.0)
-                      if (overlap and self.world > 1 and not gradient_penalty) else None)
+        # (with WGAN-GP a D parameter gets a second gradient contribution from the double
+        # backward, after its first one: D's buckets then wait for the contribution count the
+        # first step observed, OverlappedGradSync(count_accumulate=True))
+        self.dsync = (OverlappedGradSync(self.fD, process_group, bucket_mb / 4.0, count_accumulate=gradient_penalty)
+                      if (overlap and self.world > 1) else None)
+        # the next step's D(real) forward / backward (it depends on the updated D,
+        # not on the new G) runs under the G gradients' last buckets and G's Adam; on by default
+        # in data-parallel runs, where that tail is the all-reduce's
+        self.real_ahead = (self.world > 1) if real_ahead is None else bool(real_ahead)
+        self._d_real_next = None
         self._capturing = False
+        self._segmented = False
         self.identity_fn = identity_fn
         self.sync.broadcast(self.fG)
         self.sync.broadcast(self.fD)
@@ -379,26 +440,56 @@ class TPGANTrainer:
     def _phase_a(self, b):
         G, D = self.G, self.D
         self.fG.zero_grad()
-        self.fD.zero_grad()
+        # D(real) of this batch already ran at the end of the previous step (_real_ahead): its
+        # gradient is in fD.grad and its output is kept for the loss
+        d_real_pre, self._d_real_next = self._d_real_next, None
+        if d_real_pre is not None and d_real_pre[0] is not b["frontal"]:
+            d_real_pre = None  # (the caller's next batch was not the one it announced)
+        if d_real_pre is None:
+            self.fD.zero_grad()
         # the identity loss's real-image features run on a side stream under G's forward
+        # (not while phase A is captured as a graph of its own: the fork would stay unjoined
+        # at the end of that capture, and phase B's graph would wait on work of another graph)
         pre = getattr(self.identity_fn, "real_features_async", None)
+        if self._capturing and self._segmented:
+            pre = None
         self._id_pre = pre(b["frontal"]) if pre is not None else None
         with tpgan_ops.compute_dtype(self.dtype):
-            outs = G(b["I128"], b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], self.use_dropout)
+            with tpgan_ops.roctx_range("G-fwd"):
+                outs = G(b["I128"], b["left_eye"], b["right_eye"], b["nose"], b["mouth"], b["z"], self.use_dropout)
             fake = outs[0]
             B = fake.shape[0]
-            # ---- D-step (critic on real and detached fake as one 2B batch)
-            real = tpgan_ops.to_cl(b["frontal"], self.dtype)
-            d_both = D(torch.cat([real, fake.detach()], 0)).float()
-            d_real, d_fake = d_both[:B], d_both[B:]
-            loss_D = d_fake.mean() - d_real.mean()
-            if self.gp:
-                loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
-            if self.dsync is not None and not self._capturing:
-                self.dsync.begin()
-            with tpgan_ops.wgrad_side_stream():  # (weight gradients overlap the next input gradients)
-                (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
+            with tpgan_ops.roctx_range("D-step"):
+                real = tpgan_ops.to_cl(b["frontal"], self.dtype)
+                if d_real_pre is None:
+                    # ---- D-step (critic on real and detached fake as one 2B batch)
+                    d_both = D(torch.cat([real, fake.detach()], 0)).float()
+                    d_real, d_fake = d_both[:B], d_both[B:]
+                else:
+                    d_real, d_fake = d_real_pre[1], D(fake.detach()).float()
+                loss_D = d_fake.mean() - d_real.mean()
+                if self.gp:
+                    loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
+                if self.dsync is not None and not self._capturing:
+                    self.dsync.begin()
+                with tpgan_ops.wgrad_side_stream():  # (weight gradients overlap the next input gradients)
+                    (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
+
+    def _real_ahead(self, nb):
+        """The next step's D(real) forward and backward of -mean D(real) into a fresh fD.grad
+        (SURVEY.md §8e): it needs the D this step's Adam produced, not the new G, so it runs
+        while G's last gradient buckets are still being reduced and before G's Adam.  Phase A of
+        the next step adds D(fake)'s gradient to it (the same sum as the 2B critic batch)."""
+        if nb is None or not self.real_ahead or self._capturing:
+            return
+        with tpgan_ops.roctx_range("D-real-ahead"), tpgan_ops.compute_dtype(self.dtype):
+            self.fD.zero_grad()
+            d_real = self.D(tpgan_ops.to_cl(nb["frontal"], self.dtype)).float()
+            loss = -d_real.mean()
+            with tpgan_ops.wgrad_side_stream():
+                (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
+        self._d_real_next = (nb["frontal"], d_real.detach())
 
     def gradient_penalty(self, real, fake, alpha=None):
         """WGAN-GP (config.py:72 weight_gradient_penalty): mean over the batch of
@@ -419,7 +510,8 @@ class TPGANTrainer:
         D = self.D
         fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = self._st.pop("outs")
         with tpgan_ops.compute_dtype(self.dtype):
-            self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale)
+            self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
+                         check_finite=self.loss_scale != 1.0)
             # ---- G-step through the frozen, updated D
             set_requires_grad(D.parameters(), False)
             d_gen = D(fake).float()
@@ -438,7 +530,7 @@ class TPGANTrainer:
             loss_G = loss_G + w["weight_identity_preserving"] * l_ip
         if self.gsync is not None and not self._capturing:
             self.gsync.begin()
-        with tpgan_ops.wgrad_side_stream():
+        with tpgan_ops.roctx_range("G-bwd"), tpgan_ops.wgrad_side_stream():
             (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
         self._st["loss_G"] = loss_G.detach()
 
@@ -459,7 +551,9 @@ class TPGANTrainer:
                 w["weight_cross_entropy"] * l_ce)
 
     def _phase_c(self, b):
-        self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale)
+        with tpgan_ops.roctx_range("G-adam"):
+            self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
+                         check_finite=self.loss_scale != 1.0)
         return {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
 
     # ---- checkpoint / resume.  Files and formats of the reference's
@@ -507,11 +601,13 @@ class TPGANTrainer:
         import os
         if self.world > 1:  # the writer's files are complete before anyone reads
             dist.barrier(group=self.sync.group)
-        out = None
+        # every file is read and checked before anything is restored: a mismatch (in either
+        # network) leaves the trainer exactly as it was
+        loaded, adopt = [], {}
         for tag, net, flat in self._nets():
             ck = torch.load(os.path.join(dir, tag, "optimizer_epoch_%s.pth" % epoch), map_location="cpu",
                             weights_only=True)
-            hp = flat.load_optimizer_state_dict(ck["optimizer"])
+            _, hp = flat.check_optimizer_state_dict(ck["optimizer"])
             mine = {"lr": self.lr, "betas": tuple(self.betas), "eps": 1e-8, "weight_decay": 0.0}
             bad = {k: (hp[k], mine[k]) for k in hp if k in mine and not _hp_equal(hp[k], mine[k])}
             fixed = {k: v for k, v in bad.items() if k in ("eps", "weight_decay")}
@@ -519,19 +615,40 @@ class TPGANTrainer:
                 raise ValueError("checkpoint %s/%s optimizer hyperparameters differ from the trainer's "
                                  "(stored, trainer): %s" % (tag, epoch, bad))
             if bad:
-                self.lr = float(hp.get("lr", self.lr))
-                self.betas = tuple(hp.get("betas", self.betas))
+                if adopt and any(not _hp_equal(adopt[k], hp[k]) for k in adopt if k in hp):
+                    raise ValueError("checkpoint %s: G and D were saved with different hyperparameters" % epoch)
+                adopt.update({k: hp[k] for k in ("lr", "betas") if k in hp})
+            own = net.state_dict()
+            sd = ck["model"]
+            if set(sd) != set(own):
+                raise ValueError("checkpoint %s/%s: state_dict keys differ (missing %s, unexpected %s)" %
+                                 (tag, epoch, sorted(set(own) - set(sd))[:5], sorted(set(sd) - set(own))[:5]))
+            for k, v in sd.items():
+                if tuple(v.shape) != tuple(own[k].shape):
+                    raise ValueError("checkpoint %s/%s: %s has shape %s, model %s" %
+                                     (tag, epoch, k, tuple(v.shape), tuple(own[k].shape)))
+            loaded.append((net, flat, ck))
+        if adopt:
+            self.lr = float(adopt.get("lr", self.lr))
+            self.betas = tuple(adopt.get("betas", self.betas))
+        out = None
+        for net, flat, ck in loaded:
+            flat.load_optimizer_state_dict(ck["optimizer"])
             net.load_state_dict(ck["model"])  # copies into the flat-buffer views
             flat.weights_loaded()
             out = ck["epoch"]
         return out  # every rank reads the same files: replicas stay identical without a broadcast
 
-    def step(self, b):
-        """One eager G+D train step."""
+    def step(self, b, next_b=None):
+        """One eager G+D train step.  next_b: the batch of the following step, when known --
+        its D(real) pass then runs under this step's G-gradient all-reduce tail (real_ahead)."""
         self._phase_a(b)
-        self._allreduce(self.fD)
+        with tpgan_ops.roctx_range("allreduce-D"):
+            self._allreduce(self.fD)
         self._phase_b(b)
-        self._allreduce(self.fG)
+        self._real_ahead(next_b)
+        with tpgan_ops.roctx_range("allreduce-G"):
+            self._allreduce(self.fG)
         return self._phase_c(b)
 
     def capture(self, b, warmup=3, segmented=None):
@@ -544,14 +661,19 @@ class TPGANTrainer:
         self._static = {k: v.clone() for k, v in b.items()}
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        # the data-parallel bucket layout is re-learned after the first overlapped step
+        # (FlatParams.relayout moves every parameter, gradient and packed weight image): that
+        # step must run before capture, or the graphs would keep the old buffers' addresses
+        pending = any(s is not None and not s.order_learned for s in (self.gsync, self.dsync))
         with torch.cuda.stream(side):
-            for _ in range(warmup):
+            for _ in range(max(warmup, 1 if pending else 0)):
                 self.step(self._static)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if segmented is None:
             segmented = self.world > 1
         self._capturing = True  # graph replays reduce G in one call between phases
+        self._segmented = bool(segmented)
         phases = (self._phase_a, self._phase_b, self._phase_c)
         self._graphs = []
         if not segmented:
@@ -569,10 +691,17 @@ class TPGANTrainer:
                 pool = g.pool()
                 self._graphs.append(g)
         self._graph_out = out
+        self._graph_layout = (self.fG.layout_version, self.fD.layout_version)
         torch.cuda.synchronize()
 
     def step_graphed(self, b=None):
-        """One train step by graph replay (capture() first)."""
+        """One train step by graph replay (capture() first).  Returns the step's losses as
+        fresh tensors: the graph's own outputs live in its memory pool and the next replay
+        overwrites them, so a caller holding step k's dict would otherwise read step k+1's
+        values (round 2's graphed-loss experiment returned such aliased outputs)."""
+        if (self.fG.layout_version, self.fD.layout_version) != self._graph_layout:
+            raise RuntimeError("the parameters were re-laid out after capture(): the graphs hold the old buffers; "
+                               "capture() again")
         if b is not None and b is not self._static:
             for k, v in b.items():
                 self._static[k].copy_(v, non_blocking=True)
@@ -585,7 +714,7 @@ class TPGANTrainer:
             gb.replay()
             self._allreduce(self.fG)
             gc.replay()
-        return self._graph_out
+        return {k: v.clone() for k, v in self._graph_out.items()}
 
 
 def synthetic_batch(B, device, seed=0, img_size=128):
