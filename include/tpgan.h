@@ -154,6 +154,19 @@ int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, tpg_t
                        tpg_tensor g, tpg_tensor dx, tpg_tensor dw, float* dbias, void* ws, size_t ws_bytes,
                        tpg_stream_t stream);
 
+/* Launch groups (the four LocalPathways of D_and_G_model.py:18-110 run layer by layer in
+ * lockstep, replacing four per-patch launches per op with one).  Between begin and end, the
+ * calling thread's conv / activation-backward calls record their kernels instead of launching
+ * them; tpg_group_member() opens the next member (one independent problem, e.g. one patch's
+ * tpg_conv2d_fwd or tpg_conv2d_bwd).  tpg_group_end() launches the record: where every member
+ * issued the same kernel sequence, one grid per position covers all members, otherwise the
+ * launches run one by one in call order.  A call that needs another kernel flushes the record
+ * first, so the semantics are always those of the calls run in order.  Tensors and workspaces
+ * of the recorded calls must stay allocated until tpg_group_end returns. */
+void tpg_group_begin(void);
+void tpg_group_member(void);
+int32_t tpg_group_end(void);
+
 /* g = gy * act'(y) over logical [n, c, h, w]; dbias[c] += sum g (dbias may be NULL). */
 int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
                     tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, tpg_stream_t stream);

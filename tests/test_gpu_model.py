@@ -338,3 +338,88 @@ def test_generator_256_fp16_vs_fp32(gpu):
     x, y = g16["I128"].grad.double().reshape(-1), g32["I128"].grad.double().reshape(-1)
     assert bool(torch.isfinite(x).all())
     assert float(torch.dot(x, y) / (x.norm() * y.norm())) > 0.99
+
+
+# ---- launch groups (tpg_group_begin / tpg_group_end): the four LocalPathways in lockstep ----
+@pytest.mark.parametrize("dtype,flat", [(torch.bfloat16, True), (torch.float16, False), (torch.bfloat16, False)])
+def test_local_pathways_grouped_equal_per_patch(gpu, dtype, flat):
+    """LocalPathway.forward_group (one grouped node per layer: one grid per kernel position over
+    the four patches of different sizes) against the per-patch modules on the same weights and
+    inputs.  Deterministic mode (no split-K / pixel-split atomics): each member runs the same
+    kernel code with the same tiles and splits either way, so outputs, the patch gradients
+    and every parameter gradient are bit-identical.  flat: FlatParams-managed (pre-packed
+    weights, dW / db accumulated into the flat gradient buffer, GradLink shortcut hand-off)."""
+    import D_and_G_model as DG
+    import tpgan_ops
+    import tpgan_train
+    torch.manual_seed(11)
+    paths = torch.nn.ModuleList([DG.LocalPathway(use_batchnorm=False) for _ in range(4)]).to(gpu)
+    fl = tpgan_train.FlatParams(paths, gpu) if flat else None
+    B = 6
+    xs = [torch.randn(B, 3, h, w, device=gpu) for h, w in ((40, 40), (40, 40), (32, 40), (32, 48))]
+    proj = [(torch.randn(B, 3, h, w, device=gpu), torch.randn(B, 64, h, w, device=gpu))
+            for h, w in ((40, 40), (40, 40), (32, 40), (32, 48))]
+
+    def run(group):
+        if fl is not None:
+            fl.zero_grad()
+        else:
+            paths.zero_grad(set_to_none=True)
+        xin = [x.clone().requires_grad_(True) for x in xs]
+        old, tune = tpgan_ops.GROUP["enabled"], tpgan_ops.AUTOTUNE["enabled"]
+        tpgan_ops.GROUP["enabled"] = group
+        tpgan_ops.AUTOTUNE["enabled"] = False  # (both runs on the default weight-gradient tiles)
+        try:
+            with tpgan_ops.compute_dtype(dtype), tpgan_ops.deterministic():
+                outs = (DG.LocalPathway.forward_group(list(paths), xin) if group else
+                        [p(x) for p, x in zip(paths, xin)])
+                loss = 0
+                for (img, feat), (pi, pf) in zip(outs, proj):
+                    loss = loss + (img.float() * pi).sum() + (feat.float() * pf).sum()
+                loss.backward()
+        finally:
+            tpgan_ops.GROUP["enabled"] = old
+            tpgan_ops.AUTOTUNE["enabled"] = tune
+        torch.cuda.synchronize()
+        return ([o.detach().clone() for pair in outs for o in pair], [x.grad.clone() for x in xin],
+                [p.grad.detach().clone() for p in paths.parameters()])
+
+    a, b = run(True), run(False)
+    for u, v in zip(a[0], b[0]):
+        assert u.dtype == dtype and torch.equal(u, v)
+    for u, v in zip(a[1], b[1]):
+        assert torch.equal(u, v)
+    for (name, _), u, v in zip(paths.named_parameters(), a[2], b[2]):
+        assert torch.equal(u, v), name
+        assert bool(torch.isfinite(u).all()) and float(u.abs().max()) > 0, name
+
+
+def test_local_pathways_grouped_nondeterministic(gpu):
+    """Default (split) mode: grouped and per-patch runs agree to summation-order rounding."""
+    import D_and_G_model as DG
+    import tpgan_ops
+    torch.manual_seed(12)
+    paths = torch.nn.ModuleList([DG.LocalPathway(use_batchnorm=False) for _ in range(4)]).to(gpu)
+    xs = [torch.randn(16, 3, h, w, device=gpu) for h, w in ((40, 40), (40, 40), (32, 40), (32, 48))]
+
+    def run(group):
+        paths.zero_grad(set_to_none=True)
+        old = tpgan_ops.GROUP["enabled"]
+        tpgan_ops.GROUP["enabled"] = group
+        try:
+            with tpgan_ops.compute_dtype(torch.bfloat16):
+                outs = (DG.LocalPathway.forward_group(list(paths), xs) if group else
+                        [p(x) for p, x in zip(paths, xs)])
+                loss = sum(img.float().square().mean() + feat.float().mean() for img, feat in outs)
+                loss.backward()
+        finally:
+            tpgan_ops.GROUP["enabled"] = old
+        torch.cuda.synchronize()
+        return [o.detach().float() for pair in outs for o in pair], [p.grad.detach().clone() for p in paths.parameters()]
+
+    a, b = run(True), run(False)
+    for u, v in zip(a[0], b[0]):
+        assert rel(u.cpu(), v.cpu()) < 1e-2
+    ga = torch.cat([g.reshape(-1) for g in a[1]]).double()
+    gb = torch.cat([g.reshape(-1) for g in b[1]]).double()
+    assert rel(ga.cpu(), gb.cpu()) < 2e-2

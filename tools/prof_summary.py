@@ -79,8 +79,8 @@ def main():
         busy / 1e6 / steps, (span - busy) / 1e6 / steps,
         ", ".join("%s %.2f ms" % (k, v / 1e6 / steps) for k, v in sorted(gaps.items()))))
     items = sorted(agg.items(), key=lambda kv: -kv[1][1])
-    print("steps in window: %d   kernel time %.2f ms/step   wall span %.2f ms/step   (busy %.1f%%)" % (
-        steps, total / 1e6 / steps, span / 1e6 / steps, 100 * total / max(span, 1)))
+    print("steps in window: %d   kernel time %.2f ms/step   wall span %.2f ms/step   (busy %.1f%%)   launches %.0f/step" % (
+        steps, total / 1e6 / steps, span / 1e6 / steps, 100 * total / max(span, 1), len(rows) / steps))
     print("%-90s %7s %10s %9s %6s" % ("kernel", "calls", "ms/step", "avg_us", "%"))
     for k, (n, t, mx, mn) in items[:a.top]:
         print("%-90s %7d %10.3f %9.1f %6.2f" % (k, n, t / 1e6 / steps, t / n / 1e3, 100 * t / total))

@@ -14,7 +14,7 @@ import torch.nn as nn
 
 import tpgan_ops
 from ModificationLayer import *  # noqa: F401,F403  (conv, deconv, sequential, ResidualBlock, ...)
-from ModificationLayer import ResidualBlock, conv, deconv, sequential
+from ModificationLayer import ResidualBlock, conv, deconv, group_forward, sequential
 from UtilityMethods import elementwise_multiply_and_cast_to_int as EMaC2I
 
 
@@ -66,6 +66,28 @@ class LocalPathway(nn.Module):
         local_img = self.local_img(after_select2)
         assert local_img.shape == x.shape, "{} {}".format(local_img.shape, x.shape)
         return local_img, deconv2
+
+    @staticmethod
+    def forward_group(paths, xs):
+        """[p.forward(x) for p, x in zip(paths, xs)] in lockstep: each layer of the four
+        pathways runs as one grouped node (ModificationLayer.group_forward), one launch per
+        kernel instead of one per patch."""
+        G = group_forward
+        cat = tpgan_ops.cat
+        conv0 = G([p.conv0 for p in paths], xs)
+        conv1 = G([p.conv1 for p in paths], conv0)
+        conv2 = G([p.conv2 for p in paths], conv1)
+        conv3 = G([p.conv3 for p in paths], conv2)
+        deconv0 = G([p.deconv0 for p in paths], conv3)
+        after_select0 = G([p.after_select0 for p in paths], [cat([a, b]) for a, b in zip(deconv0, conv2)])
+        deconv1 = G([p.deconv1 for p in paths], after_select0)
+        after_select1 = G([p.after_select1 for p in paths], [cat([a, b]) for a, b in zip(deconv1, conv1)])
+        deconv2 = G([p.deconv2 for p in paths], after_select1)
+        after_select2 = G([p.after_select2 for p in paths], [cat([a, b]) for a, b in zip(deconv2, conv0)])
+        local_img = G([p.local_img for p in paths], after_select2)
+        for img, x in zip(local_img, xs):
+            assert img.shape == x.shape, "{} {}".format(img.shape, x.shape)
+        return list(zip(local_img, deconv2))
 
 
 class LocalFuser(nn.Module):
@@ -267,7 +289,21 @@ class Generator(nn.Module):
         paths = (self.local_pathway_left_eye, self.local_pathway_right_eye, self.local_pathway_nose,
                  self.local_pathway_mouth)
         patches = (left_eye, right_eye, nose, mouth)
-        if tpgan_ops.MULTISTREAM and I128.is_cuda:
+        if tpgan_ops.GROUP["enabled"] and I128.is_cuda:
+            # the four local pathways in lockstep on one side stream (one grouped launch per
+            # layer and kernel), concurrently with the global pathway's local-independent part
+            main = torch.cuda.current_stream()
+            st = tpgan_ops.side_streams(I128.device, 1, "local")[0] if tpgan_ops.MULTISTREAM else main
+            st.wait_stream(main)
+            with torch.cuda.stream(st), tpgan_ops.concurrent(tpgan_ops.MULTISTREAM):
+                outs = LocalPathway.forward_group(paths, patches)
+            enc = self.global_pathway.encode(I128, z)
+            if st is not main:
+                main.wait_stream(st)
+                for img, feat in outs:
+                    img.record_stream(main)
+                    feat.record_stream(main)
+        elif tpgan_ops.MULTISTREAM and I128.is_cuda:
             # The four local pathways (small maps: kernels that fill few CUs) run on their
             # own HIP streams, concurrently with the global pathway's local-independent part
             # on the current stream; autograd replays each op's backward on its forward

@@ -118,6 +118,86 @@ def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=N
                             link_res=link_res, link_dx=link_dx, **_conv_geom_args(layer, pad_mod))
 
 
+def _conv_call(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None):
+    """tpgan_ops.conv2d keyword arguments of _apply_conv's call, or None where it would not
+    call conv2d (dilated / grouped convs)."""
+    if tuple(layer.dilation) != (1, 1) or layer.groups != 1:
+        return None
+    if (isinstance(layer, nn.Conv2d) and layer.in_channels <= 4 and residual is None and link_dx is None and
+            pad_mod is None and layer.padding_mode == "zeros" and layer.kernel_size != (1, 1)):
+        ph, pw = layer.padding
+        a = tpgan_ops.folded_args(x, layer.weight, tuple(layer.stride), (ph, ph, pw, pw))
+        if a is not None:
+            a.update(bias=layer.bias, act=act)
+            return a
+    return dict(x=x, weight=layer.weight, bias=layer.bias, act=act, residual=residual, res_scale=res_scale,
+                link_res=link_res, link_dx=link_dx, **_conv_geom_args(layer, pad_mod))
+
+
+def group_forward(mods, xs):
+    """mods[k](xs[k]) for same-structured modules (the four LocalPathways' copies of one
+    layer), in lockstep: each fused conv of the structure runs as ONE grouped node over all k
+    (tpgan_ops.conv2d_group: one launch per kernel position instead of one per module).
+    Structures it does not know run module by module."""
+    m0 = mods[0]
+    if all(isinstance(m, _FusedSequential) for m in mods):
+        parts = [m._parts() for m in mods]
+        if all(p is not None for p in parts):
+            return _group_fused(mods, xs)
+        kids = [list(m._modules.values()) for m in mods]
+        if (all(p is None for p in parts) and all(len(k) == len(kids[0]) for k in kids) and
+                all(isinstance(c, (_FusedSequential, ResidualBlock)) for c in kids[0])):
+            for i in range(len(kids[0])):
+                xs = group_forward([k[i] for k in kids], xs)
+            return xs
+    elif all(isinstance(m, ResidualBlock) for m in mods) and all(type(m) is type(m0) for m in mods):
+        out = _group_resblock(mods, xs)
+        if out is not None:
+            return out
+    return [m(x) for m, x in zip(mods, xs)]
+
+
+def _group_fused(seqs, xs, residuals=None, res_scales=None, post_acts=None, links_res=None, links_dx=None):
+    n = len(seqs)
+    calls = []
+    for k, (seq, x) in enumerate(zip(seqs, xs)):
+        pad, layer, act = seq._parts()
+        residual = residuals[k] if residuals is not None else None
+        if residual is not None:
+            if act is not None:
+                raise RuntimeError("residual fusion expects a conv without activation")
+            act = post_acts[k]
+        c = _conv_call(layer, x, pad, act, residual, res_scales[k] if res_scales is not None else 1.0,
+                       links_res[k] if links_res is not None else None, links_dx[k] if links_dx is not None else None)
+        if c is None:
+            return [seq(x, residual=(residuals[k] if residuals is not None else None),
+                        res_scale=(res_scales[k] if res_scales is not None else 1.0),
+                        post_act=(post_acts[k] if post_acts is not None else None),
+                        link_res=(links_res[k] if links_res is not None else None),
+                        link_dx=(links_dx[k] if links_dx is not None else None)) for k, (seq, x) in enumerate(zip(seqs, xs))]
+        calls.append(c)
+    assert len(calls) == n
+    return tpgan_ops.conv2d_group(calls)
+
+
+def _group_resblock(blocks, xs):
+    """ResidualBlock.forward over the group; None where the block is not the fused form."""
+    b0 = blocks[0]
+    layers = [list(b.layers) for b in blocks]
+    if (len(layers[0]) < 2 or any(len(b.shortcut._modules) for b in blocks) or
+            tpgan_ops.act_code(b0.activation) is None or
+            any(l[-1]._parts() is None or any(m._parts() is None for m in l[:-1]) for l in layers)):
+        return None
+    links = None
+    if tpgan_ops.RES_LINK["enabled"] and torch.is_grad_enabled() and all(_link_ok(l[0]) for l in layers):
+        links = [tpgan_ops.GradLink() for _ in blocks]
+    h = xs
+    for i in range(len(layers[0]) - 1):
+        h = _group_fused([l[i] for l in layers], h, links_dx=links if i == 0 else None)
+    return _group_fused([l[-1] for l in layers], h, residuals=xs, res_scales=[b.scaling_factor for b in blocks],
+                        post_acts=[b.activation for b in blocks], links_res=links)
+
+
 def _link_ok(seq):
     """seq is a fused [conv] [act] whose input gradient can take a parked gradient (GradLink)."""
     parts = seq._parts() if isinstance(seq, _FusedSequential) else None

@@ -81,6 +81,182 @@ static int32_t hip_check(int e, const char* what) {
   return fail(e > 0 ? e : -100, "%s failed: %s", what, e > 0 ? hipGetErrorString((hipError_t)e) : "bad config");
 }
 
+// ------------------------------------------------------------------ launch groups --
+// Between tpg_group_begin and tpg_group_end the halo conv, its split-K epilogue, the
+// tap-flattened weight gradient and the vector activation backward are recorded instead of
+// launched, tagged with the member (tpg_group_member) whose call issued them.  At the end,
+// when every member issued the same sequence of kernel instances, position j of all members
+// runs as ONE grouped launch (tpg_internal.h Grouped); otherwise, and for anything a member
+// launches outside those four kernels (which first flushes the record), the launches run
+// one by one in their original order.  Members must be independent of each other.
+struct GLaunch {
+  int kind;  // 1 halo, 2 epilogue, 3 wgrad2, 4 act_bwd (vector form)
+  int member;
+  hipStream_t s;
+  int dtype, cfg, bm, bn;
+  bool mask;
+  HaloArgs h;
+  EpiArgs e;
+  Wgrad2Args w;
+  ActVecArgs v;
+};
+struct GroupRec {
+  bool active = false;
+  int member = 0;
+  std::vector<GLaunch> q;
+};
+static thread_local GroupRec g_grp;
+
+static int run_one(const GLaunch& L) {
+  switch (L.kind) {
+    case 1: return launch_halo(L.h, L.dtype, L.cfg, L.s, L.mask);
+    case 2: return launch_epilogue(L.e, L.s);
+    case 3: return launch_wgrad2(L.w, L.dtype, L.cfg, L.bm, L.bn, L.s);
+    default: return launch_act_vec(L.v, L.dtype, L.s);
+  }
+}
+
+// run the recorded launches one by one, in order (the record stays active)
+static int group_flush() {
+  if (!g_grp.active || g_grp.q.empty()) return 0;
+  int rc = 0;
+  for (const GLaunch& L : g_grp.q)
+    if (!rc) rc = run_one(L);
+  g_grp.q.clear();
+  return rc;
+}
+
+// same kernel instance up to what a grouped launch adapts per member (the halo kernel's halo
+// capacity class: the grouped launch takes the largest the members need)
+static bool same_instance(const GLaunch& a, const GLaunch& b) {
+  if (a.kind != b.kind || a.s != b.s || a.dtype != b.dtype || a.mask != b.mask) return false;
+  if (a.kind == 1) return (a.cfg >= 40) == (b.cfg >= 40) && (a.cfg >= 40 ? a.cfg == b.cfg : a.cfg % 8 == b.cfg % 8);
+  return a.cfg == b.cfg && a.bm == b.bm && a.bn == b.bn;
+}
+
+// Members run their own launches in order; across members any interleaving is valid.  Each
+// round takes the first unfinished member's next launch and groups it with every other
+// member whose next launch is the same instance.
+static int group_run_merged() {
+  std::vector<std::vector<const GLaunch*>> by(std::max(g_grp.member, 0) + 1);
+  for (const GLaunch& L : g_grp.q) by[L.member].push_back(&L);
+  by.erase(std::remove_if(by.begin(), by.end(), [](const std::vector<const GLaunch*>& v) { return v.empty(); }),
+           by.end());
+  const int nmem = (int)by.size();
+  std::vector<size_t> head(nmem, 0);
+  int rc = 0;
+  for (;;) {
+    int lead = -1;
+    for (int m = 0; m < nmem && lead < 0; ++m)
+      if (head[m] < by[m].size()) lead = m;
+    if (lead < 0) break;
+    const GLaunch& L0 = *by[lead][head[lead]];
+    std::vector<int> mem;
+    for (int m = lead; m < nmem && (int)mem.size() < TPG_GROUP_MAX; ++m)
+      if (head[m] < by[m].size() && same_instance(*by[m][head[m]], L0)) mem.push_back(m);
+    const int n = (int)mem.size();
+    int r = -1;
+    if (n >= 2) {
+      if (L0.kind == 1) {
+        HaloArgs a[TPG_GROUP_MAX];
+        for (int k = 0; k < n; ++k) a[k] = by[mem[k]][head[mem[k]]]->h;
+        r = launch_halo_group(a, n, L0.dtype, L0.cfg, L0.s, L0.mask);
+      } else if (L0.kind == 2) {
+        EpiArgs a[TPG_GROUP_MAX];
+        for (int k = 0; k < n; ++k) a[k] = by[mem[k]][head[mem[k]]]->e;
+        r = launch_epilogue_group(a, n, L0.s);
+      } else if (L0.kind == 3) {
+        Wgrad2Args a[TPG_GROUP_MAX];
+        for (int k = 0; k < n; ++k) a[k] = by[mem[k]][head[mem[k]]]->w;
+        r = launch_wgrad2_group(a, n, L0.dtype, L0.cfg, L0.bm, L0.bn, L0.s);
+      } else {
+        ActVecArgs a[TPG_GROUP_MAX];
+        for (int k = 0; k < n; ++k) a[k] = by[mem[k]][head[mem[k]]]->v;
+        r = launch_act_vec_group(a, n, L0.dtype, L0.s);
+      }
+    }
+    if (r == -1) {  // a single member, or no grouped build of this instance: one by one
+      r = 0;
+      for (int k = 0; k < n && !r; ++k) r = run_one(*by[mem[k]][head[mem[k]]]);
+    }
+    if (r && !rc) rc = r;
+    for (int k = 0; k < n; ++k) ++head[mem[k]];
+  }
+  g_grp.q.clear();
+  return rc;
+}
+
+static GLaunch& grec(int kind, hipStream_t s, int dtype) {
+  g_grp.q.emplace_back();
+  GLaunch& L = g_grp.q.back();
+  L.kind = kind; L.member = std::max(g_grp.member, 0); L.s = s; L.dtype = dtype;
+  L.cfg = L.bm = L.bn = 0; L.mask = false;
+  return L;
+}
+
+static int do_halo(const HaloArgs& h, int dtype, int cfg, hipStream_t s, bool mask) {
+  if (!g_grp.active) return launch_halo(h, dtype, cfg, s, mask);
+  GLaunch& L = grec(1, s, dtype);
+  L.h = h; L.cfg = cfg; L.mask = mask;
+  return 0;
+}
+static int do_epilogue(const EpiArgs& e, hipStream_t s) {
+  if (!g_grp.active) return launch_epilogue(e, s);
+  GLaunch& L = grec(2, s, e.dtype);
+  L.e = e;
+  return 0;
+}
+static int do_wgrad2(const Wgrad2Args& w, int dtype, int cfg, int bm, int bn, hipStream_t s) {
+  if (!g_grp.active || !w.bflat) {
+    const int rc = group_flush();
+    return rc ? rc : launch_wgrad2(w, dtype, cfg, bm, bn, s);
+  }
+  GLaunch& L = grec(3, s, dtype);
+  L.w = w; L.cfg = cfg; L.bm = bm; L.bn = bn;
+  return 0;
+}
+
+// any other launch: the recorded ones go first
+#define TPG_GROUP_SYNC()             \
+  do {                               \
+    const int grc_ = group_flush();  \
+    if (grc_) return hip_check(grc_, "group flush"); \
+  } while (0)
+
+static int do_act_bwd(int n, int c, int h, int w, int act, float slope, const tpg_tensor& gy, const tpg_tensor& y,
+                      const tpg_tensor& g, float* dbias, hipStream_t s) {
+  if (g_grp.active) {
+    ActVecArgs v;
+    if (act_vec_args(n, c, h, w, act, slope, gy, y, g, dbias, &v) == 0) {
+      GLaunch& L = grec(4, s, g.dtype);
+      L.v = v;
+      return 0;
+    }
+    const int rc = group_flush();
+    if (rc) return rc;
+  }
+  return tpg_act_bwd_impl(n, c, h, w, act, slope, gy, y, g, dbias, s);
+}
+
+extern "C" void tpg_group_begin(void) {
+  group_flush();
+  g_grp.active = true;
+  g_grp.member = -1;
+  g_grp.q.clear();
+}
+
+extern "C" void tpg_group_member(void) {
+  if (g_grp.active) ++g_grp.member;
+}
+
+extern "C" int32_t tpg_group_end(void) {
+  if (!g_grp.active) return 0;
+  const int rc = g_grp.q.empty() ? 0 : group_run_merged();
+  g_grp.active = false;
+  g_grp.q.clear();
+  return hip_check(rc, "grouped launch");
+}
+
 static inline int esize(int dtype) { return dtype == TPG_F32 ? 4 : 2; }
 static inline bool half16(int dtype) { return dtype == TPG_BF16 || dtype == TPG_F16; }  // 16-bit MFMA operands
 static inline int64_t rup(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
@@ -609,6 +785,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     if (P.halo) {
       HaloArgs& h = P.h;
       if (h.ntaps > 0 && !packed) {
+        TPG_GROUP_SYNC();
         int e = launch_pack_halo(k, h.nks, h.BN, h.ntiles, s);
         if (e) return hip_check(e, "pack_halo");
       }
@@ -627,7 +804,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
         h.M = mk->M.data; h.m_sn = mk->M.stride[0]; h.m_sh = mk->M.stride[2]; h.m_sw = mk->M.stride[3];
         h.G = mk->G.data; h.mact = mk->act; h.mslope = mk->slope;
       }
-      int e = launch_halo(h, dtype, P.hcfg, s, mk != nullptr);
+      int e = do_halo(h, dtype, P.hcfg, s, mk != nullptr);
       if (e) return hip_check(e, "halo conv");
       if (h.ksplit > 1) {
         EpiArgs ep;
@@ -639,11 +816,12 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
         ep.bias = bias; ep.bias_mod = 0;
         ep.R = R.data; ep.r_sn = R.stride[0]; ep.r_sh = R.stride[2]; ep.r_sw = R.stride[3];
         ep.res_scale = res_scale; ep.act = act; ep.slope = slope; ep.dtype = dtype;
-        e = launch_epilogue(ep, s);
+        e = do_epilogue(ep, s);
         if (e) return hip_check(e, "halo epilogue");
       }
       continue;
     }
+    TPG_GROUP_SYNC();
     if (a.nunits > 0 && !packed) {
       int e = launch_pack(k, s);
       if (e) return hip_check(e, "pack");
@@ -753,6 +931,7 @@ extern "C" int64_t tpg_pack_prepare(void* jobs, int32_t n) {
 }
 
 extern "C" int32_t tpg_pack_run(const void* jobs_dev, int32_t n, int64_t nblocks, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (n <= 0) return 0;
   if (!jobs_dev || nblocks <= 0 || nblocks >= (1ll << 31)) return fail(-2, "pack_run: bad batch");
   return hip_check(launch_pack_many(reinterpret_cast<const PackJob*>(jobs_dev), n, (int)nblocks, (hipStream_t)stream),
@@ -816,6 +995,7 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
   rc = run_probs(v, d->dtype, g, w, nullptr, 0, none, 0.f, tmp, TPG_ACT_NONE, 0.f, reinterpret_cast<char*>(ws) + tmpb,
                  ws_bytes - tmpb, s, pk);
   if (rc) return rc;
+  TPG_GROUP_SYNC();
   return hip_check(launch_reflect_fold(d->n, d->in_c, d->in_h, d->in_w, d->pad_t, d->pad_b, d->pad_l, d->pad_r, tmp, dx, s),
                    "reflect_fold");
 }
@@ -904,6 +1084,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   // bias MFMAs spread over up to 16 / ksplit tiles: same-address atomics serialise (~50 ns
   // each), so blocks x splits adding into one dbias row must stay few
   a.bshare = deterministic() ? 1 : std::max(1, std::min(a.ntb * a.nrg * cdiv(a.kw, a.nt), 16 / a.ksplit));
+  TPG_GROUP_SYNC();
   return hip_check(launch_wgrad_rh(a, stream), "wgrad_rh");
 }
 
@@ -1026,7 +1207,7 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
       a.dpx = kp % a.PW;
       a.dbias = dbias;
       a.bshare = deterministic() ? 1 : std::max(1, std::min((int)((ncols + bn - 1) / bn) * ngrid, 16 / a.ksplit));
-      const int32_t r2 = hip_check(launch_wgrad2(a, d->dtype, wgrad2_cfg(bm, bn), bm, bn, (hipStream_t)stream), "wgrad2");
+      const int32_t r2 = hip_check(do_wgrad2(a, d->dtype, wgrad2_cfg(bm, bn), bm, bn, (hipStream_t)stream), "wgrad2");
       *bias_done = r2 == 0 && dbias != nullptr;
       return r2;
     }
@@ -1039,6 +1220,7 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
   if (deterministic()) ks = 1;
   a.pix_per_split = (int)rup(cdiv(a.npix, ks), 32);
   a.ksplit = cdiv(a.npix, a.pix_per_split);
+  TPG_GROUP_SYNC();
   return hip_check(launch_wgrad(a, d->dtype, cfg, (hipStream_t)stream), "wgrad");
 }
 
@@ -1109,7 +1291,7 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
     // (ConvTranspose2d: its weight-gradient kernels never take the bias -- it would cost a
     // separate column-sum launch, so this pass keeps it)
     float* db = (dw.data && !d->transposed) ? nullptr : dbias;
-    rc = hip_check(tpg_act_bwd_impl(d->n, d->out_c, d->out_h, d->out_w, d->act, d->slope, gy, y, g, db, s),
+    rc = hip_check(do_act_bwd(d->n, d->out_c, d->out_h, d->out_w, d->act, d->slope, gy, y, g, db, s),
                    "act_bwd");
     if (rc) return rc;
     have_g = true;
@@ -1124,19 +1306,23 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
     if ((rc = bwd_filter_impl(d, x, G, dw, bias_done ? nullptr : dbias, &b, stream))) return rc;
     bias_done = bias_done || b;
   }
-  if (dbias && !bias_done)
+  if (dbias && !bias_done) {
+    TPG_GROUP_SYNC();
     return hip_check(tpg_colsum_impl(d->n, d->out_c, d->out_h, d->out_w, G, dbias, s), "colsum");
+  }
   return 0;
 }
 
 extern "C" int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope, tpg_tensor gy,
                                tpg_tensor y, tpg_tensor g, float* dbias, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (!gy.data || !g.data || (act != TPG_ACT_NONE && !y.data)) return fail(-10, "act_bwd: NULL tensor");
   return hip_check(tpg_act_bwd_impl(n, c, h, w, act, slope, gy, y, g, dbias, (hipStream_t)stream), "act_bwd");
 }
 
 extern "C" int32_t tpg_copy4d(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor in, tpg_tensor out,
                               tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (!in.data || !out.data) return fail(-10, "copy4d: NULL tensor");
   if ((int64_t)n * c * h * w == 0) return 0;
   return hip_check(tpg_copy4d_impl(n, c, h, w, in, out, (hipStream_t)stream), "copy4d");
@@ -1145,6 +1331,7 @@ extern "C" int32_t tpg_copy4d(int32_t n, int32_t c, int32_t h, int32_t w, tpg_te
 extern "C" int32_t tpg_fold_taps(int32_t n, int32_t c, int32_t h, int32_t w, int32_t fh, int32_t fw, int32_t sh,
                                  int32_t sw, int32_t pt, int32_t pl, int32_t oh, int32_t ow, tpg_tensor x, tpg_tensor y,
                                  int32_t backward, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (!x.data || !y.data) return fail(-10, "fold_taps: NULL tensor");
   if (fh < 1 || fw < 1 || sh < 1 || sw < 1 || n < 0 || c < 1 || (int64_t)fh * fw * c > 4096)
     return fail(-2, "fold_taps: bad geometry");
@@ -1156,6 +1343,7 @@ extern "C" int32_t tpg_fold_taps(int32_t n, int32_t c, int32_t h, int32_t w, int
 extern "C" int32_t tpg_local_fuse_fwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, const tpg_tensor* parts,
                                       const int32_t* ph, const int32_t* pw, const int32_t* top, const int32_t* left,
                                       tpg_tensor y, uint8_t* argmax, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   for (int k = 0; k < 4; ++k)
     if (!parts[k].data) return fail(-10, "local_fuse: part %d NULL", k);
   return hip_check(tpg_fuse_fwd_impl(n, c, out_h, out_w, parts, ph, pw, top, left, y, argmax, (hipStream_t)stream),
@@ -1165,6 +1353,7 @@ extern "C" int32_t tpg_local_fuse_fwd(int32_t n, int32_t c, int32_t out_h, int32
 extern "C" int32_t tpg_local_fuse_bwd(int32_t n, int32_t c, int32_t out_h, int32_t out_w, tpg_tensor gy,
                                       const uint8_t* argmax, const tpg_tensor* dparts, const int32_t* ph,
                                       const int32_t* pw, const int32_t* top, const int32_t* left, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (!argmax || !gy.data) return fail(-10, "local_fuse_bwd: NULL");
   return hip_check(tpg_fuse_bwd_impl(n, c, out_h, out_w, gy, argmax, dparts, ph, pw, top, left, (hipStream_t)stream),
                    "local_fuse_bwd");
@@ -1172,17 +1361,20 @@ extern "C" int32_t tpg_local_fuse_bwd(int32_t n, int32_t c, int32_t out_h, int32
 
 extern "C" int32_t tpg_maxout2_fwd(int32_t b, int32_t m, tpg_tensor x, tpg_tensor y, uint8_t* argmax,
                                    tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   return hip_check(tpg_maxout_fwd_impl(b, m, x, y, argmax, (hipStream_t)stream), "maxout_fwd");
 }
 
 extern "C" int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argmax, tpg_tensor dx,
                                    tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   return hip_check(tpg_maxout_bwd_impl(b, m, gy, argmax, dx, (hipStream_t)stream), "maxout_bwd");
 }
 
 extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                             float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                             float grad_scale, float* state, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (numel == 0) return 0;
   if (!param || !grad || !exp_avg || !exp_avg_sq || !state) return fail(-10, "adam: NULL pointer");
   if (step < 0) return fail(-2, "adam: step must be >= 0");
@@ -1195,6 +1387,7 @@ extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, floa
 extern "C" int32_t tpg_grad_check_impl(int64_t, const float*, float*, hipStream_t);
 
 extern "C" int32_t tpg_grad_check(int64_t numel, const float* grad, float* state, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
   if (!grad || !state) return fail(-10, "grad_check: NULL pointer");
   const int rc = tpg_grad_check_impl(numel, grad, state, (hipStream_t)stream);
   if (rc == -1) return fail(-15, "grad_check: gradient buffer must be 16-byte aligned");

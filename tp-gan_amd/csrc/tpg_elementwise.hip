@@ -5,6 +5,8 @@
 #include "tpg_internal.h"
 #include "../../include/tpgan.h"
 #include <stdlib.h>
+#include <string.h>
+#include <algorithm>
 
 namespace tpg {
 
@@ -169,10 +171,22 @@ __global__ __launch_bounds__(256) void act_bwd_rows_kernel(int64_t npix, int C, 
 // pixels per iteration with all loads issued before any use (HBM latency hiding).  Its
 // dbias partials stay in registers; the block combines them through LDS (no LDS atomics)
 // and adds one global atomic per channel, with at most 1024 blocks per launch.
-template <typename E>
-__global__ __launch_bounds__(256) void act_bwd_vec_kernel(int64_t npix, int C, int act, float slope, const E* gy,
-                                                          int64_t gps, const E* y, int64_t yps, E* g, int64_t gps_out,
-                                                          float* dbias, int64_t pix_per_block) {
+template <typename E, int NG = 1>
+__global__ __launch_bounds__(256) void act_bwd_vec_kernel(const Grouped<ActVecArgs, NG> G) {
+  int mem = 0, bid = blockIdx.x;
+  if constexpr (NG > 1) {  // grouped: member blocks [boff[m], boff[m + 1])
+    mem = group_member(G, blockIdx.x);
+    bid = blockIdx.x - G.boff[mem];
+  }
+  const ActVecArgs& a = G.a[mem];
+  const int64_t npix = a.npix, pix_per_block = a.pix_per_block;
+  const int C = a.C, act = a.act;
+  const float slope = a.slope;
+  const E* gy = reinterpret_cast<const E*>(a.gy);
+  const E* y = reinterpret_cast<const E*>(a.y);
+  E* g = reinterpret_cast<E*>(a.g);
+  const int64_t gps = a.gps, yps = a.yps, gps_out = a.gps_out;
+  float* dbias = a.dbias;
   constexpr int EPC = 16 / sizeof(E);
   constexpr int U = 4;
   __shared__ float sb[256 * EPC];
@@ -184,7 +198,7 @@ __global__ __launch_bounds__(256) void act_bwd_vec_kernel(int64_t npix, int C, i
 #pragma unroll
   for (int e = 0; e < EPC; ++e) part[e] = 0.f;
   const int c0 = ch * EPC;
-  const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
+  const int64_t p0 = (int64_t)bid * pix_per_block;
   const int64_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
   const bool has_act = act != TPG_ACT_NONE;
   if (active) {
@@ -600,36 +614,76 @@ static bool pix_dense_vec(const tpg_tensor& t, int h, int w, int dtype, int c) {
   return ((uintptr_t)t.data % 16) == 0;
 }
 
+namespace tpg {
+// vector form plan: >= 4 pixels per lane (one unrolled iteration: small maps get enough
+// blocks to hide the load latency), <= 1024 blocks (bounds the dbias atomics per channel);
+// deterministic mode with a bias gradient: one block, so every dbias element gets ONE atomic
+// add (a fixed-order sum)
+int act_vec_plan(int64_t npix, int c, int dtype, bool dbias, ActVecArgs* a) {
+  memset(a, 0, sizeof(*a));
+  const int epc = dtype != TPG_F32 ? 8 : 4;
+  const int ppi = 256 / ((c + epc - 1) / epc);
+  const int64_t blocks = (dbias && deterministic()) ? 1 :
+      std::max<int64_t>(1, std::min<int64_t>((npix + act_ppl() * ppi - 1) / (act_ppl() * ppi), act_cap()));
+  a->npix = npix;
+  a->C = c;
+  a->pix_per_block = (npix + blocks - 1) / blocks;
+  a->blocks = (int)blocks;
+  return 0;
+}
+
+// the vector form's arguments when it applies (0), else 1
+int act_vec_args(int n, int c, int h, int w, int act, float slope, const tpg_tensor& gy, const tpg_tensor& y,
+                 const tpg_tensor& g, float* dbias, ActVecArgs* a) {
+  const int dt = g.dtype;
+  const int epc = dt != TPG_F32 ? 8 : 4;
+  if (!(c <= 1024 && (c + epc - 1) / epc <= 256 && pix_dense_vec(gy, h, w, dt, c) && pix_dense_vec(g, h, w, dt, c) &&
+        (act == TPG_ACT_NONE || pix_dense_vec(y, h, w, dt, c))))
+    return 1;
+  act_vec_plan((int64_t)n * h * w, c, dt, dbias != nullptr, a);
+  a->act = act; a->slope = slope;
+  a->gy = gy.data; a->gps = gy.stride[3]; a->y = y.data; a->yps = y.stride[3]; a->g = g.data; a->gps_out = g.stride[3];
+  a->dbias = dbias;
+  return 0;
+}
+
+template <int NG>
+static void launch_act_vec_t(const Grouped<ActVecArgs, NG>& g, int blocks, int dtype, hipStream_t s) {
+  if (dtype == TPG_F16) hipLaunchKernelGGL((act_bwd_vec_kernel<_Float16, NG>), dim3(blocks), dim3(256), 0, s, g);
+  else if (dtype == TPG_BF16) hipLaunchKernelGGL((act_bwd_vec_kernel<__bf16, NG>), dim3(blocks), dim3(256), 0, s, g);
+  else if constexpr (NG == 1) hipLaunchKernelGGL((act_bwd_vec_kernel<float, NG>), dim3(blocks), dim3(256), 0, s, g);
+}
+
+int launch_act_vec(const ActVecArgs& a, int dtype, hipStream_t s) {
+  Grouped<ActVecArgs, 1> g;
+  g.a[0] = a; g.boff[0] = 0; g.boff[1] = a.blocks; g.nm = 1;
+  launch_act_vec_t<1>(g, a.blocks, dtype, s);
+  return (int)hipGetLastError();
+}
+
+int launch_act_vec_group(const ActVecArgs* a, int n, int dtype, hipStream_t s) {
+  if (n < 2 || n > TPG_GROUP_MAX || (dtype != TPG_BF16 && dtype != TPG_F16)) return -1;
+  Grouped<ActVecArgs, TPG_GROUP_MAX> g;
+  memset(&g, 0, sizeof(g));
+  int blocks = 0;
+  for (int m = 0; m < n; ++m) {
+    g.a[m] = a[m];
+    g.boff[m] = blocks;
+    blocks += a[m].blocks;
+  }
+  g.boff[n] = blocks;
+  g.nm = n;
+  launch_act_vec_t<TPG_GROUP_MAX>(g, blocks, dtype, s);
+  return (int)hipGetLastError();
+}
+}  // namespace tpg
+
 extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
                                      tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, hipStream_t s) {
   const int dt = g.dtype;
-  const int epc = dt != TPG_F32 ? 8 : 4;
   static const bool force_scalar = getenv("TPG_ACTB_SCALAR") != nullptr;  // debug switch
-  if (!force_scalar && c <= 1024 && (c + epc - 1) / epc <= 256 && pix_dense_vec(gy, h, w, dt, c) && pix_dense_vec(g, h, w, dt, c) &&
-      (act == TPG_ACT_NONE || pix_dense_vec(y, h, w, dt, c))) {
-    const int64_t npix = (int64_t)n * h * w;
-    const int ppi = 256 / ((c + epc - 1) / epc);
-    // >= 4 pixels per lane (one unrolled iteration: small maps get enough blocks to hide the
-    // load latency), <= 1024 blocks (bounds the dbias atomics per channel)
-    // deterministic mode with a bias gradient: one block, so every dbias element gets ONE
-    // atomic add (a fixed-order sum)
-    const int64_t blocks = (dbias && deterministic()) ? 1 :
-        std::max<int64_t>(1, std::min<int64_t>((npix + act_ppl() * ppi - 1) / (act_ppl() * ppi), act_cap()));
-    const int64_t ppb = (npix + blocks - 1) / blocks;
-    if (dt == TPG_F16)
-      hipLaunchKernelGGL(act_bwd_vec_kernel<_Float16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
-                         (const _Float16*)gy.data, gy.stride[3], (const _Float16*)y.data, y.stride[3], (_Float16*)g.data,
-                         g.stride[3], dbias, ppb);
-    else if (dt == TPG_BF16)
-      hipLaunchKernelGGL(act_bwd_vec_kernel<__bf16>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
-                         (const __bf16*)gy.data, gy.stride[3], (const __bf16*)y.data, y.stride[3], (__bf16*)g.data,
-                         g.stride[3], dbias, ppb);
-    else
-      hipLaunchKernelGGL(act_bwd_vec_kernel<float>, dim3((int)blocks), dim3(256), 0, s, npix, c, act, slope,
-                         (const float*)gy.data, gy.stride[3], (const float*)y.data, y.stride[3], (float*)g.data,
-                         g.stride[3], dbias, ppb);
-    return (int)hipGetLastError();
-  }
+  ActVecArgs a;
+  if (!force_scalar && act_vec_args(n, c, h, w, act, slope, gy, y, g, dbias, &a) == 0) return launch_act_vec(a, dt, s);
   int64_t npix = (int64_t)n * h * w;
   if (!force_scalar && c <= 256 && pix_dense_any(gy, h, w) && pix_dense_any(g, h, w) &&
       (act == TPG_ACT_NONE || pix_dense_any(y, h, w))) {

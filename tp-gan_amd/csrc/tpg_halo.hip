@@ -26,6 +26,7 @@
 #include <type_traits>
 #include <algorithm>
 #include <stdlib.h>
+#include <string.h>
 
 namespace tpg {
 
@@ -75,8 +76,24 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
   return a.u;
 }
 
-template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256>
-__global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
+template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
+__global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> GA) {
+  // block -> (member, x = sub-tile group, y = N-tile, z = k split); a grouped grid is 1-D in
+  // the plain grid's dispatch order (x fastest) within each member
+  int mem = 0, bx, by, bz;
+  if constexpr (NG == 1) {
+    bx = blockIdx.x; by = blockIdx.y; bz = blockIdx.z;
+  } else {
+    mem = group_member(GA, blockIdx.x);
+    const HaloArgs& q = GA.a[mem];
+    const int l = blockIdx.x - GA.boff[mem];
+    const int gx = (q.N * q.tiles_h * q.tiles_w + q.IMG - 1) / q.IMG;
+    const int yz = l / gx;
+    bx = l - yz * gx;
+    bz = yz / q.ntiles;
+    by = yz - bz * q.ntiles;
+  }
+  const HaloArgs& p = GA.a[mem];
   using E = dt_t<DT>;
   constexpr bool BF = DT != 0;  // 16-bit operands (bf16 or fp16)
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk
@@ -104,9 +121,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   const int HW = p.HW, HP = p.HH * HW;                 // halo pixels of one sub-tile
   const int tiles = p.tiles_h * p.tiles_w, tiles_w = p.tiles_w;
   const int ntot = p.N * tiles;                        // sub-tiles in the grid
-  const int st0 = blockIdx.x * IMG;
-  const int n0 = blockIdx.y * BN;
-  const int z = blockIdx.z;
+  const int st0 = bx * IMG;
+  const int n0 = by * BN;
+  const int z = bz;
   const int ks0 = z * p.kps;
   const int nks = min(p.nks, ks0 + p.kps) - ks0;
   const E* Ag = reinterpret_cast<const E*>(p.A);
@@ -114,7 +131,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
   // packed weights: Wp[step][ntile][BNL][4 chunks]; this wave streams GL KiB of each slice
   const int64_t wstep = (int64_t)p.ntiles * BNL * 64;
   const char* wsrc = reinterpret_cast<const char*>(p.Wp) + (int64_t)ks0 * p.ntaps * wstep +
-                     (int64_t)blockIdx.y * BNL * 64 + (wave * GL * 1024 + lane * 16);
+                     (int64_t)by * BNL * 64 + (wave * GL * 1024 + lane * 16);
 
   // ---- per-thread halo slots (fixed across k-steps): element offset from A (absolute,
   // < 2^31 by the planner), negative = outside the image or a dead sub-tile -> zero
@@ -149,7 +166,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const HaloArgs p) {
           if constexpr (MASK) {
             mpix[q] = (int)((int64_t)nimg * p.m_sn + gy * p.m_sh + gx * p.m_sw);
             const int cy = gy - ty * TH, cx = gx - tx * TW;  // (SH = SW = 1 in this mode)
-            if (blockIdx.y == 0 && (unsigned)cy < (unsigned)TH && (unsigned)cx < (unsigned)TW) core |= 1u << q;
+            if (by == 0 && (unsigned)cy < (unsigned)TH && (unsigned)cx < (unsigned)TW) core |= 1u << q;
           }
         }
       }
@@ -584,16 +601,24 @@ size_t halo_lds_bytes(int hcap, int bn, int rs, int bm) {
   return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn, bm));
 }
 
-template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256>
-static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
-  auto k = halo_kernel<DT, HL, BN, WM, WN, MASK, BM>;
-  const size_t lds = halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3, BM);
+template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
+static int launch_halo_t(const Grouped<HaloArgs, NG>& g, dim3 grid, size_t lds, hipStream_t s) {
+  auto k = halo_kernel<DT, HL, BN, WM, WN, MASK, BM, NG>;
   const int maxl = (int)halo_lds_bytes(HL * 128, BN, HL == 8 ? 3 : 4, BM);  // (1024-pixel halos: 3-slot ring only)
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
                       true);
   (void)once;
-  hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);
+  hipLaunchKernelGGL(k, grid, dim3(512), lds, s, g);
   return (int)hipGetLastError();
+}
+
+template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256>
+static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
+  Grouped<HaloArgs, 1> g;
+  g.a[0] = a;
+  g.boff[0] = 0; g.boff[1] = (int)(grid.x * grid.y * grid.z); g.nm = 1;
+  return launch_halo_t<DT, HL, BN, WM, WN, MASK, BM, 1>(g, grid, halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3, BM),
+                                                        s);
 }
 
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask) {
@@ -630,6 +655,62 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
                       : launch_halo_t<0, HL_, BN_, WM_, WN_, false>(a, grid, s);           \
   }
   TPG_HALO_CFGS_S2(X)
+#undef X
+  return -1;
+}
+
+// Grouped builds (16-bit operands, 256-row tiles): the channel widths of the LocalPathway
+// layers (32 / 64 / 128-column tiles: 3, 64, 128, 256 and 512 channels) at every halo size,
+// and their stride-2 convs.  {id, HL, BN, WM, WN, mask variant}
+#define TPG_HALO_GROUP_CFGS(X) \
+  X(0, 3, 32, 8, 1, true)      \
+  X(1, 3, 64, 8, 1, true)      \
+  X(3, 3, 128, 4, 2, true)     \
+  X(8, 4, 32, 8, 1, true)      \
+  X(9, 4, 64, 8, 1, true)      \
+  X(11, 4, 128, 4, 2, true)    \
+  X(16, 5, 32, 8, 1, true)     \
+  X(17, 5, 64, 8, 1, true)     \
+  X(19, 5, 128, 4, 2, true)    \
+  X(40, 8, 32, 8, 1, false)    \
+  X(41, 8, 64, 8, 1, false)    \
+  X(43, 8, 128, 4, 2, false)
+
+int launch_halo_group(const HaloArgs* a, int n, int dtype, int cfg, hipStream_t s, bool mask) {
+  if (n < 2 || n > TPG_GROUP_MAX || (dtype != 1 && dtype != 2)) return -1;
+  Grouped<HaloArgs, TPG_GROUP_MAX> g;
+  memset(&g, 0, sizeof(g));
+  size_t lds = 0;
+  int hcap = 0, blocks = 0;
+  for (int m = 0; m < n; ++m) {
+    const HaloArgs& h = a[m];
+    if (h.BN != a[0].BN || (h.var & 2) || h.var != a[0].var) return -1;
+    if (mask && (h.ntaps < 2 || h.hcap % 16 || h.SH != 1 || h.SW != 1)) return -1;
+    g.a[m] = h;
+    g.boff[m] = blocks;
+    blocks += ((h.N * h.tiles_h * h.tiles_w + h.IMG - 1) / h.IMG) * h.ntiles * h.ksplit;
+    hcap = std::max(hcap, h.hcap);
+    lds = std::max(lds, halo_lds_bytes(h.hcap, h.BN, 3, 256));
+  }
+  g.boff[n] = blocks;
+  g.nm = n;
+  // the halo capacity class every member fits (members differ in map size / tile)
+  if (cfg < 24) cfg = halo_cfg(std::max(3, (hcap * 4 + 511) / 512), a[0].BN);
+  if (cfg < 0) return -1;
+  const dim3 grid(blocks);
+#define X(id, HL_, BN_, WM_, WN_, MK_)                                                                  \
+  if (cfg == (id)) {                                                                                    \
+    if (hcap > HL_ * 128 || (mask && !MK_)) return -1;                                                  \
+    if (mask) {                                                                                         \
+      if constexpr (MK_)                                                                                \
+        return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, MK_, 256, TPG_GROUP_MAX>(g, grid, lds, s) \
+                          : launch_halo_t<2, HL_, BN_, WM_, WN_, MK_, 256, TPG_GROUP_MAX>(g, grid, lds, s); \
+      return -1;                                                                                        \
+    }                                                                                                   \
+    return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, false, 256, TPG_GROUP_MAX>(g, grid, lds, s)  \
+                      : launch_halo_t<2, HL_, BN_, WM_, WN_, false, 256, TPG_GROUP_MAX>(g, grid, lds, s); \
+  }
+  TPG_HALO_GROUP_CFGS(X)
 #undef X
   return -1;
 }

@@ -27,6 +27,8 @@
 // space instead; tpg_epilogue_kernel finishes them.
 #include "tpg_internal.h"
 #include <type_traits>
+#include <algorithm>
+#include <string.h>
 
 namespace tpg {
 
@@ -261,14 +263,21 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmArgs p) {
 
 // Split-K finalize: v = sum of the partial slices (+ bias, + residual, activation).
 // V columns per thread (4 when Nout % 4 == 0: 16-byte slice reads).
-template <typename E, int V>
-__global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs p) {
+template <typename E, int V, int NG = 1>
+__global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG> G) {
+  int mem = 0;
+  int64_t b0 = blockIdx.x, nb = gridDim.x;
+  if constexpr (NG > 1) {  // grouped: member blocks [boff[m], boff[m + 1])
+    mem = group_member(G, blockIdx.x);
+    b0 = blockIdx.x - G.boff[mem];
+    nb = G.boff[mem + 1] - G.boff[mem];
+  }
+  const EpiArgs& p = G.a[mem];
   const int64_t total = (int64_t)p.M * p.Nout / V;
   const int JHJW = p.JH * p.JW;
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t idx = b0 * blockDim.x + threadIdx.x; idx < total; idx += nb * blockDim.x) {
     const int64_t e0 = idx * V;
     int row = (int)(e0 / p.Nout);
     int col = (int)(e0 - (int64_t)row * p.Nout);
@@ -337,21 +346,45 @@ int launch_igemm(const IgemmArgs& a, int dtype, int cfg, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+static bool epi_v4(const EpiArgs& a) { return a.Nout % 4 == 0 && ((uintptr_t)a.ws % 16) == 0 && a.slice % 4 == 0; }
+static int epi_blocks(const EpiArgs& a, bool v4) {
+  const int64_t total = (int64_t)a.M * a.Nout / (v4 ? 4 : 1);
+  return (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
+}
+
+template <typename E, int NG>
+static void launch_epi_t(const Grouped<EpiArgs, NG>& g, bool v4, int blocks, hipStream_t s) {
+  if (v4) hipLaunchKernelGGL((epilogue_kernel<E, 4, NG>), dim3(blocks), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((epilogue_kernel<E, 1, NG>), dim3(blocks), dim3(256), 0, s, g);
+}
+
 int launch_epilogue(const EpiArgs& a, hipStream_t s) {
-  const bool v4 = a.Nout % 4 == 0 && ((uintptr_t)a.ws % 16) == 0 && a.slice % 4 == 0;
-  int64_t total = (int64_t)a.M * a.Nout / (v4 ? 4 : 1);
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-  if (blocks < 1) blocks = 1;
-  if (a.dtype == 2) {
-    if (v4) hipLaunchKernelGGL((epilogue_kernel<_Float16, 4>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((epilogue_kernel<_Float16, 1>), dim3(blocks), dim3(256), 0, s, a);
-  } else if (a.dtype == 1) {
-    if (v4) hipLaunchKernelGGL((epilogue_kernel<__bf16, 4>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((epilogue_kernel<__bf16, 1>), dim3(blocks), dim3(256), 0, s, a);
-  } else {
-    if (v4) hipLaunchKernelGGL((epilogue_kernel<float, 4>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((epilogue_kernel<float, 1>), dim3(blocks), dim3(256), 0, s, a);
+  const bool v4 = epi_v4(a);
+  const int blocks = epi_blocks(a, v4);
+  Grouped<EpiArgs, 1> g;
+  g.a[0] = a; g.boff[0] = 0; g.boff[1] = blocks; g.nm = 1;
+  if (a.dtype == 2) launch_epi_t<_Float16, 1>(g, v4, blocks, s);
+  else if (a.dtype == 1) launch_epi_t<__bf16, 1>(g, v4, blocks, s);
+  else launch_epi_t<float, 1>(g, v4, blocks, s);
+  return (int)hipGetLastError();
+}
+
+int launch_epilogue_group(const EpiArgs* a, int n, hipStream_t s) {
+  if (n < 2 || n > TPG_GROUP_MAX || (a[0].dtype != 1 && a[0].dtype != 2)) return -1;
+  const bool v4 = epi_v4(a[0]);
+  Grouped<EpiArgs, TPG_GROUP_MAX> g;
+  memset(&g, 0, sizeof(g));
+  int blocks = 0;
+  for (int m = 0; m < n; ++m) {
+    if (a[m].dtype != a[0].dtype || epi_v4(a[m]) != v4) return -1;
+    g.a[m] = a[m];
+    g.boff[m] = blocks;
+    blocks += epi_blocks(a[m], v4);
   }
+  g.boff[n] = blocks;
+  g.nm = n;
+  if (a[0].dtype == 2) launch_epi_t<_Float16, TPG_GROUP_MAX>(g, v4, blocks, s);
+  else launch_epi_t<__bf16, TPG_GROUP_MAX>(g, v4, blocks, s);
   return (int)hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include "../../include/tpgan.h"
 
 #define TPG_MAX_TAPS 64
 
@@ -352,6 +353,55 @@ struct HaloArgs {
   float mslope;
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
+
+// ---------------------------------------------------------------- grouped launches ----
+// One grid over up to TPG_GROUP_MAX independent problems of the same kernel instance (the
+// four LocalPathways' same-shaped layers, tpg_group_begin / tpg_group_end): member m owns
+// the 1-D blocks [boff[m], boff[m + 1]) and reads its own argument block a[m].  NG = 1 is the
+// plain launch (the kernel keeps its own grid shape).
+#define TPG_GROUP_MAX 4
+template <typename A, int NG>
+struct Grouped {
+  A a[NG];
+  int boff[NG + 1];
+  int nm;
+};
+template <typename A, int NG>
+__device__ __forceinline__ int group_member(const Grouped<A, NG>& G, int bid) {
+  int m = 0;
+#pragma unroll
+  for (int i = 1; i < NG; ++i)
+    if (i < G.nm && bid >= G.boff[i]) m = i;
+  return m;
+}
+
+// g = gy * act'(y) (+ dbias column sums), vector form: pixel-dense channels-last rows, 16-byte
+// aligned (tpg_elementwise.hip act_bwd_vec_kernel)
+struct ActVecArgs {
+  int64_t npix;
+  int C, act;
+  float slope;
+  const void* gy;
+  int64_t gps;
+  const void* y;
+  int64_t yps;
+  void* g;
+  int64_t gps_out;
+  float* dbias;
+  int64_t pix_per_block;
+  int blocks;
+};
+
+// Grouped launchers: return -1 (nothing launched) when the instance has no grouped build or
+// the members disagree on it; the caller then launches the members one by one.
+int launch_halo_group(const HaloArgs* a, int n, int dtype, int cfg, hipStream_t s, bool mask);
+int launch_epilogue_group(const EpiArgs* a, int n, hipStream_t s);
+int launch_wgrad2_group(const Wgrad2Args* a, int n, int dtype, int cfg, int bm, int bn, hipStream_t s);
+int act_vec_plan(int64_t npix, int c, int dtype, bool dbias, ActVecArgs* out);
+int act_vec_args(int n, int c, int h, int w, int act, float slope, const ::tpg_tensor& gy, const ::tpg_tensor& y,
+                 const ::tpg_tensor& g, float* dbias, ActVecArgs* a);
+int launch_act_vec(const ActVecArgs& a, int dtype, hipStream_t s);
+int launch_act_vec_group(const ActVecArgs* a, int n, int dtype, hipStream_t s);
 
 // sets the thread-local message returned by tpg_last_error() (tpg_capi.hip); returns code
 int record_error(int code, const char* msg);

@@ -16,6 +16,7 @@
 // that are never written.
 #include "tpg_internal.h"
 #include <type_traits>
+#include <string.h>
 
 namespace tpg {
 
@@ -48,8 +49,16 @@ __device__ __forceinline__ int w2_swz(int row) {
   }
 }
 
-template <int DT, int BM, int BN, int WM, int WN, bool FLAT>
-__global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
+template <int DT, int BM, int BN, int WM, int WN, bool FLAT, int NG = 1>
+__global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, NG> G) {
+  // grouped launch: member m owns blocks [boff[m], boff[m + 1]) (its own 1-D grid)
+  int mem = 0, bid0 = blockIdx.x, nblk0 = gridDim.x;
+  if constexpr (NG > 1) {
+    mem = group_member(G, blockIdx.x);
+    bid0 = blockIdx.x - G.boff[mem];
+    nblk0 = G.boff[mem + 1] - G.boff[mem];
+  }
+  const Wgrad2Args& p = G.a[mem];
   using E = dt_t<DT>;
   constexpr bool BF = DT != 0;
   constexpr int ES = sizeof(E);
@@ -72,8 +81,8 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Wgrad2Args p) {
   // share a pixel range (same dY rows, X rows shifted by the taps) meet in one L2.
   const int nta = (p.Ca + BM - 1) / BM;
   const int ntb = ((FLAT ? p.ntaps * p.cbp : p.Cb) + BN - 1) / BN;
-  const int nblk = gridDim.x, full = nblk & ~7;
-  const int bid = blockIdx.x;
+  const int nblk = nblk0, full = nblk & ~7;
+  const int bid = bid0;
   const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
   const int tile = L % (nta * ntb), rest = L / (nta * ntb);
   const int ta = tile % nta, tb = tile / nta;
@@ -410,30 +419,32 @@ int wgrad2_cfg(int bm, int bn) {
   return -1;
 }
 
+static int w2_blocks(const Wgrad2Args& a, int bm, int bn) {
+  const int ncols = a.bflat ? a.ntaps * a.cbp : a.Cb;
+  return ((a.Ca + bm - 1) / bm) * ((ncols + bn - 1) / bn) * (a.bflat ? 1 : a.ntaps) * a.ksplit;
+}
+
+template <int DT, int BM, int BN, int WM, int WN, bool FLAT, int NG>
+static int launch_w2_k(const Grouped<Wgrad2Args, NG>& g, int blocks, hipStream_t s) {
+  auto k = wgrad2_kernel<DT, BM, BN, WM, WN, FLAT, NG>;
+  const size_t lds = 3 * (DT ? 64 * (BM + BN) * 2 : 32 * (BM + BN) * 4);
+  static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                      true);
+  (void)once;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, s, g);
+  return (int)hipGetLastError();
+}
+
 template <bool FLAT>
 static int launch_wgrad2_t(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s) {
-  const int ncols = FLAT ? a.ntaps * a.cbp : a.Cb;
-  dim3 grid(((a.Ca + bm - 1) / bm) * ((ncols + bn - 1) / bn) * (FLAT ? 1 : a.ntaps) * a.ksplit);
+  Grouped<Wgrad2Args, 1> g;
+  g.a[0] = a;
+  g.boff[0] = 0; g.boff[1] = w2_blocks(a, bm, bn); g.nm = 1;
 #define X(id, BM_, BN_, WM_, WN_)                                                                       \
   if (cfg == (id)) {                                                                                    \
-    if (dtype != 0) {                                                                                   \
-      auto k = dtype == 2 ? wgrad2_kernel<2, BM_, BN_, WM_, WN_, FLAT> : wgrad2_kernel<1, BM_, BN_, WM_, WN_, FLAT>; \
-      const size_t lds = 3 * 64 * (BM_ + BN_) * 2;                                                      \
-      static bool once1 = ((void)hipFuncSetAttribute((const void*)wgrad2_kernel<1, BM_, BN_, WM_, WN_, FLAT>, \
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true); \
-      static bool once2 = ((void)hipFuncSetAttribute((const void*)wgrad2_kernel<2, BM_, BN_, WM_, WN_, FLAT>, \
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true); \
-      (void)once1; (void)once2;                                                                         \
-      hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                \
-    } else {                                                                                            \
-      auto k = wgrad2_kernel<0, BM_, BN_, WM_, WN_, FLAT>;                                              \
-      const size_t lds = 3 * 32 * (BM_ + BN_) * 4;                                                      \
-      static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                                    (int)lds), true);                                   \
-      (void)once;                                                                                       \
-      hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a);                                                \
-    }                                                                                                   \
-    return (int)hipGetLastError();                                                                      \
+    if (dtype == 2) return launch_w2_k<2, BM_, BN_, WM_, WN_, FLAT, 1>(g, g.boff[1], s);               \
+    if (dtype == 1) return launch_w2_k<1, BM_, BN_, WM_, WN_, FLAT, 1>(g, g.boff[1], s);               \
+    return launch_w2_k<0, BM_, BN_, WM_, WN_, FLAT, 1>(g, g.boff[1], s);                               \
   }
   TPG_WGRAD2_CFGS(X)
 #undef X
@@ -442,6 +453,30 @@ static int launch_wgrad2_t(const Wgrad2Args& a, int dtype, int cfg, int bm, int 
 
 int launch_wgrad2(const Wgrad2Args& a, int dtype, int cfg, int bm, int bn, hipStream_t s) {
   return a.bflat ? launch_wgrad2_t<true>(a, dtype, cfg, bm, bn, s) : launch_wgrad2_t<false>(a, dtype, cfg, bm, bn, s);
+}
+
+// grouped builds: 16-bit operands, tap-flattened columns, every tile
+int launch_wgrad2_group(const Wgrad2Args* a, int n, int dtype, int cfg, int bm, int bn, hipStream_t s) {
+  if (n < 2 || n > TPG_GROUP_MAX || (dtype != 1 && dtype != 2)) return -1;
+  Grouped<Wgrad2Args, TPG_GROUP_MAX> g;
+  memset(&g, 0, sizeof(g));
+  int blocks = 0;
+  for (int m = 0; m < n; ++m) {
+    if (!a[m].bflat) return -1;
+    g.a[m] = a[m];
+    g.boff[m] = blocks;
+    blocks += w2_blocks(a[m], bm, bn);
+  }
+  g.boff[n] = blocks;
+  g.nm = n;
+#define X(id, BM_, BN_, WM_, WN_)                                                                       \
+  if (cfg == (id)) {                                                                                    \
+    if (dtype == 2) return launch_w2_k<2, BM_, BN_, WM_, WN_, true, TPG_GROUP_MAX>(g, blocks, s);      \
+    return launch_w2_k<1, BM_, BN_, WM_, WN_, true, TPG_GROUP_MAX>(g, blocks, s);                      \
+  }
+  TPG_WGRAD2_CFGS(X)
+#undef X
+  return -1;
 }
 
 }  // namespace tpg

@@ -103,6 +103,9 @@ EXPORTS = {
                                                                    ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p,
                                                                    ctypes.c_int32, ctypes.c_void_p]),
     "tpg_set_deterministic": (None, [ctypes.c_int32]),
+    "tpg_group_begin": (None, []),
+    "tpg_group_member": (None, []),
+    "tpg_group_end": (ctypes.c_int32, []),
     "tpg_get_deterministic": (ctypes.c_int32, []),
     "tpg_version": (ctypes.c_char_p, []),
     "tpg_last_error": (ctypes.c_char_p, []),

@@ -457,6 +457,55 @@ def _ws(lib, desc, op, device):
     return torch.empty(nb, dtype=torch.uint8, device=device)
 
 
+def _conv_act_forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res=None, link_dx=None,
+                      keep=None):
+    """_ConvAct's forward on any ctx with save_for_backward (a _MemberCtx inside a grouped
+    node); keep: a list that holds every temporary a deferred (grouped) launch still reads."""
+    lib = load()
+    dtype = get_compute_dtype()
+    ctx.in_dtype = x.dtype
+    x = _fix_c1(to_cl(x, dtype))
+    n, cin, h, w = x.shape
+    if geom.transposed:
+        cin_w, cout = weight.shape[0], weight.shape[1]
+    else:
+        cout, cin_w = weight.shape[0], weight.shape[1]
+    if cin_w != cin:
+        raise RuntimeError("expected input with %d channels, got %d" % (cin_w, cin))
+    oh, ow = geom.out_hw(h, w)
+    y = new_act(n, cout, oh, ow, dtype, x.device)
+    res = None
+    if residual is not None:
+        res = _fix_c1(to_cl(residual, dtype))
+        if tuple(res.shape) != (n, cout, oh, ow):
+            raise RuntimeError("residual shape %s != output %s" % (tuple(res.shape), (n, cout, oh, ow)))
+    d = geom.desc(n, cin, h, w, cout, oh, ow, dtype, act, slope, res_scale)
+    ws = _ws(lib, d, OP_FWD, x.device)
+    wv = weight if weight.dtype == torch.float32 else weight.float()
+    FLOPS["fwd"] += _conv_flops(d)
+    e0 = _probe_begin(d, "fwd")
+    pk = _packed_weight(wparam if wparam is not None else weight, d, OP_FWD, wv)
+    bptr = bias.data_ptr() if bias is not None else None
+    _run_maybe_packed(
+        lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), _packed_tt(pk), bptr, tt(res), tt(_fix_c1(y)),
+                                   ws.data_ptr(), ws.numel(), stream_ptr()),
+        lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bptr, tt(res), tt(_fix_c1(y)),
+                                   ws.data_ptr(), ws.numel(), stream_ptr()), d, pk)
+    _probe_end(e0, d, "fwd")
+    if keep is not None:
+        keep += [ws, res, wv]
+    ctx.save_for_backward(x, weight, y)
+    ctx.geom, ctx.act, ctx.slope, ctx.res_scale = geom, act, slope, res_scale
+    ctx.has_bias, ctx.has_res = bias is not None, residual is not None
+    ctx.d = d
+    ctx.wparam = wparam if wparam is not None else weight
+    ctx.bparam = bias
+    ctx.res_dtype = residual.dtype if residual is not None else None
+    ctx.x_dtype = x.dtype
+    ctx.link_res, ctx.link_dx = link_res, link_dx
+    return y
+
+
 class _ConvAct(torch.autograd.Function):
     """y = act(conv(x, w) + b [+ res_scale * residual]) with a HIP forward, input gradient,
     weight gradient and a fused activation'/bias-gradient pass (backward reads only the
@@ -464,47 +513,8 @@ class _ConvAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res=None, link_dx=None):
-        lib = load()
-        dtype = get_compute_dtype()
-        ctx.in_dtype = x.dtype
-        x = _fix_c1(to_cl(x, dtype))
-        n, cin, h, w = x.shape
-        if geom.transposed:
-            cin_w, cout = weight.shape[0], weight.shape[1]
-        else:
-            cout, cin_w = weight.shape[0], weight.shape[1]
-        if cin_w != cin:
-            raise RuntimeError("expected input with %d channels, got %d" % (cin_w, cin))
-        oh, ow = geom.out_hw(h, w)
-        y = new_act(n, cout, oh, ow, dtype, x.device)
-        res = None
-        if residual is not None:
-            res = _fix_c1(to_cl(residual, dtype))
-            if tuple(res.shape) != (n, cout, oh, ow):
-                raise RuntimeError("residual shape %s != output %s" % (tuple(res.shape), (n, cout, oh, ow)))
-        d = geom.desc(n, cin, h, w, cout, oh, ow, dtype, act, slope, res_scale)
-        ws = _ws(lib, d, OP_FWD, x.device)
-        wv = weight if weight.dtype == torch.float32 else weight.float()
-        FLOPS["fwd"] += _conv_flops(d)
-        e0 = _probe_begin(d, "fwd")
-        pk = _packed_weight(wparam if wparam is not None else weight, d, OP_FWD, wv)
-        bptr = bias.data_ptr() if bias is not None else None
-        _run_maybe_packed(
-            lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), _packed_tt(pk), bptr, tt(res), tt(_fix_c1(y)),
-                                       ws.data_ptr(), ws.numel(), stream_ptr()),
-            lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bptr, tt(res), tt(_fix_c1(y)),
-                                       ws.data_ptr(), ws.numel(), stream_ptr()), d, pk)
-        _probe_end(e0, d, "fwd")
-        ctx.save_for_backward(x, weight, y)
-        ctx.geom, ctx.act, ctx.slope, ctx.res_scale = geom, act, slope, res_scale
-        ctx.has_bias, ctx.has_res = bias is not None, residual is not None
-        ctx.d = d
-        ctx.wparam = wparam if wparam is not None else weight
-        ctx.bparam = bias
-        ctx.res_dtype = residual.dtype if residual is not None else None
-        ctx.x_dtype = x.dtype
-        ctx.link_res, ctx.link_dx = link_res, link_dx
-        return y
+        return _conv_act_forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res,
+                                 link_dx)
 
     @staticmethod
     def backward(ctx, gy):
@@ -586,7 +596,14 @@ class _ConvAct(torch.autograd.Function):
 FUSED_BWD = {"enabled": True}
 
 
-def _conv_act_backward_fused(ctx, gy):
+def _deferred_read(what):
+    raise RuntimeError("grouped backward: %s would read a gradient whose launch is still deferred" % what)
+
+
+def _conv_act_backward_fused(ctx, gy, keep=None):
+    """keep (grouped node, inside tpg_group_begin / end): the launches are deferred, so every
+    temporary they use is appended to keep, and nothing may read their outputs here."""
+    grouped = keep is not None
     lib = load()
     x, weight, y = ctx.saved_tensors
     d = ctx.d
@@ -630,7 +647,8 @@ def _conv_act_backward_fused(ctx, gy):
     # the weight-gradient tile / split is autotuned on a shape's first call, which needs g:
     # that call runs the fused op without dW, tunes on its g, then runs the weight gradient
     key = _wgrad_key(d)
-    tune_first = (need_dw and AUTOTUNE["enabled"] and d.dtype != TPG_F32 and key not in AUTOTUNE["cache"])
+    tune_first = (need_dw and AUTOTUNE["enabled"] and d.dtype != TPG_F32 and key not in AUTOTUNE["cache"] and
+                  not grouped)
     if need_dw and not tune_first:
         d.algo, d.ksplit = AUTOTUNE["cache"].get(key, (0, 0))
     if need_dx:
@@ -647,7 +665,7 @@ def _conv_act_backward_fused(ctx, gy):
     # (a residual block's last conv parks its g for the first conv's in-place dgrad, GradLink:
     # its weight gradient stays on this stream, ahead of that write; a ConvTranspose2d sums its
     # bias in the activation-backward pass, so it stays unsplit too)
-    split = (side is not None and dwt is not None and dw is None and (dbias is None or fused_b) and
+    split = (side is not None and not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
              ctx.link_res is None and not ctx.geom.transposed and PROBE["match"] is None and
              not torch.cuda.is_current_stream_capturing())
     e0 = _probe_begin(d, "bwd")
@@ -658,6 +676,8 @@ def _conv_act_backward_fused(ctx, gy):
                                    tt(None if split else dwt), None if split else bptr, wsp, wsn, stream_ptr()), d, pk)
     _probe_end(e0, d, "bwd", _conv_flops(d) * (int(bool(need_dx)) + int(bool(need_dw and not tune_first))))
     d.flags = d.flags & ~FLAG_DX_ACCUM
+    if grouped:
+        keep += [ws, g, gy, wv]
     if split:
         gt = gy if g_is_gy else g  # (g now holds act'(y) * gy: the second call takes it as is)
         ev = torch.cuda.Event()
@@ -678,6 +698,8 @@ def _conv_act_backward_fused(ctx, gy):
         dw = None
         need_dw = False
     if acc is not None and dx is not None:  # (not accumulated in the launch: shape / dtype mismatch)
+        if grouped:
+            _deferred_read("the parked shortcut gradient's add")
         dx = dx + acc
     if tune_first:
         algo, ks = _tuned_wgrad(lib, d, x, g, dwv)
@@ -691,8 +713,12 @@ def _conv_act_backward_fused(ctx, gy):
         if dw is None:
             _grad_ready(ctx.wparam)
         elif dw.dtype != weight.dtype:
+            if grouped:
+                _deferred_read("a weight-gradient dtype cast")
             dw = dw.to(weight.dtype)
     if dx is not None and dx.dtype != ctx.in_dtype:
+        if grouped:
+            _deferred_read("an input-gradient dtype cast")
         dx = dx.to(ctx.in_dtype)
     dres = None
     if ctx.has_res and ctx.needs_input_grad[3]:
@@ -702,7 +728,11 @@ def _conv_act_backward_fused(ctx, gy):
             ctx.link_res.g = dres
             dres = None
         elif dres.dtype != ctx.res_dtype:
+            if grouped:
+                _deferred_read("a residual-gradient dtype cast")
             dres = dres.to(ctx.res_dtype)
+    if grouped and dres is not None and dres is not g and dres is not gy:
+        _deferred_read("the scaled residual gradient")
     return dx, dw, dbias, dres, None, None, None, None, None
 
 
@@ -836,7 +866,13 @@ def _conv_act_backward_graph(ctx, gy):
 GRAD_READY_HOOK = [None]
 
 
+_READY_DEFER = [None]  # inside a grouped backward: the launches are deferred, so are their ready marks
+
+
 def _grad_ready(p):
+    if _READY_DEFER[-1] is not None:
+        _READY_DEFER[-1].append(p)
+        return
     h = GRAD_READY_HOOK[0]
     if h is not None:
         h(p)
@@ -876,6 +912,98 @@ def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_Z
     geom = ConvGeom(kh, kw, stride, pad, pad_mode, transposed, output_padding)
     return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale), wparam, link_res,
                           link_dx)
+
+
+# ---- launch groups: one node for the same layer of several independent networks (the four
+# LocalPathways, D_and_G_model.py:18-110), whose forward and backward each run inside one
+# tpg_group_begin / tpg_group_end scope: every kernel position becomes ONE grid over all members
+# instead of one small launch per patch.  GROUP["enabled"] = False: per-member _ConvAct nodes.
+GROUP = {"enabled": os.environ.get("TPG_NO_GROUP") is None}
+
+
+class _MemberCtx(object):
+    """Stands in for a _ConvAct ctx inside a grouped node."""
+
+    def save_for_backward(self, *t):
+        self.saved = t
+
+
+class _ConvActGroup(torch.autograd.Function):
+    """n _ConvAct calls on independent inputs as one autograd node (see GROUP)."""
+
+    @staticmethod
+    def forward(ctx, specs, *flat):
+        lib = load()
+        keep, subs, outs = [], [], []
+        lib.tpg_group_begin()
+        try:
+            for m, sp in enumerate(specs):
+                x, w, b, r = flat[4 * m:4 * m + 4]
+                lib.tpg_group_member()
+                sc = _MemberCtx()
+                outs.append(_conv_act_forward(sc, x, w, b, r, *sp, keep=keep))
+                subs.append(sc)
+        finally:
+            rc = lib.tpg_group_end()
+        check(rc)
+        saved = []
+        for sc in subs:
+            saved += list(sc.saved)
+            sc.saved = None
+        ctx.subs = subs
+        ctx.save_for_backward(*saved)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        saved = ctx.saved_tensors
+        for m, sc in enumerate(ctx.subs):
+            sc.saved_tensors = saved[3 * m:3 * m + 3]
+            sc.needs_input_grad = tuple(ctx.needs_input_grad[1 + 4 * m:5 + 4 * m]) + (False,) * 5
+        grads = []
+        if torch.is_grad_enabled():  # create_graph (WGAN-GP): members one by one, differentiable
+            for sc, gy in zip(ctx.subs, gys):
+                grads += list(_conv_act_backward_graph(sc, gy)[:4])
+        elif FUSED_BWD["enabled"]:
+            lib = load()
+            keep, ready = [], []
+            lib.tpg_group_begin()
+            _READY_DEFER.append(ready)
+            try:
+                for sc, gy in zip(ctx.subs, gys):
+                    lib.tpg_group_member()
+                    grads += list(_conv_act_backward_fused(sc, gy, keep=keep)[:4])
+            finally:
+                _READY_DEFER.pop()
+                rc = lib.tpg_group_end()
+            check(rc)
+            for p in ready:  # (their accumulating launches are enqueued now)
+                _grad_ready(p)
+        else:
+            for sc, gy in zip(ctx.subs, gys):
+                grads += list(_ConvAct._backward_three_calls(sc, gy)[:4])
+        for sc in ctx.subs:
+            sc.saved_tensors = None
+        return (None,) + tuple(grads)
+
+
+def conv2d_group(calls):
+    """conv2d over several independent problems as one grouped node; calls = list of dicts of
+    conv2d's keyword arguments (x, weight required).  Returns the list of outputs."""
+    if not GROUP["enabled"] or len(calls) < 2:
+        return [conv2d(**c) for c in calls]
+    specs, flat = [], []
+    for c in calls:
+        code = act_code(c.get("act"))
+        if code is None:
+            raise ValueError("activation %r cannot be fused" % (c.get("act"),))
+        weight = c["weight"]
+        geom = ConvGeom(weight.shape[2], weight.shape[3], c.get("stride", (1, 1)), c.get("pad", (0, 0, 0, 0)),
+                        c.get("pad_mode", PAD_ZERO), c.get("transposed", False), c.get("output_padding", (0, 0)))
+        specs.append((geom, code[0], code[1], float(c.get("res_scale", 1.0)), c.get("wparam"), c.get("link_res"),
+                      c.get("link_dx")))
+        flat += [c["x"], weight, c.get("bias"), c.get("residual")]
+    return list(_ConvActGroup.apply(specs, *flat))
 
 
 RES_LINK = {"enabled": not os.environ.get("TPG_NO_RES_LINK")}  # (A/B, tests: off = autograd sums it)
@@ -921,14 +1049,14 @@ class _UnfoldTaps(torch.autograd.Function):
 FOLD = {"enabled": os.environ.get("TPG_NO_FOLD") is None}
 
 
-def conv2d_folded(x, weight, bias, stride, pad, act):
-    """A zero-padded Conv2d on a thin input (the 3-channel images; reference
-    ModificationLayer.py:54-123 conv() at D_and_G_model.py:33,193,415) as a conv over the
-    tap-folded input: all KHxKW taps folded (KH*KW*C <= 32: one 32-channel MFMA k-step, a 1x1
-    conv) or, at stride 1, the KW horizontal taps (a KHx1 conv on KW*C channels) -- instead
-    of KH*KW k-steps with 3 live channels of 32.  The weight is a strided view of the same
-    channels-last memory ([co][ky][kx][c] is also [co][(ky*KW+kx)*C+c]), so its gradient
-    accumulates in place.  Returns None when the shape is not covered."""
+def folded_args(x, weight, stride, pad):
+    """conv2d keyword arguments (x, weight, pad, wparam) of the tap-folded form of a zero-padded
+    Conv2d on a thin input (the 3-channel images; reference ModificationLayer.py:54-123 conv()
+    at D_and_G_model.py:33,193,415): all KHxKW taps folded (KH*KW*C <= 32: one 32-channel MFMA
+    k-step, a 1x1 conv) or, at stride 1, the KW horizontal taps (a KHx1 conv on KW*C channels)
+    -- instead of KH*KW k-steps with 3 live channels of 32.  The weight is a strided view of
+    the same channels-last memory ([co][ky][kx][c] is also [co][(ky*KW+kx)*C+c]), so its
+    gradient accumulates in place.  None when the shape is not covered."""
     if not FOLD["enabled"] or not x.is_cuda or weight.dim() != 4:
         return None
     co, c, kh, kw = weight.shape
@@ -941,12 +1069,20 @@ def conv2d_folded(x, weight, bias, stride, pad, act):
     if kh * kw * c <= 32:
         xf = _FoldTaps.apply(x, kh, kw, sh, sw, pt, pl, oh, ow)
         wf = weight.as_strided((co, kh * kw * c, 1, 1), (kh * kw * c, 1, kh * kw * c, kh * kw * c))
-        return conv2d(xf, wf, bias, act=act, wparam=weight)
+        return dict(x=xf, weight=wf, wparam=weight)
     if sh == 1 and sw == 1 and kw * c <= 32:
         xf = _FoldTaps.apply(x, 1, kw, 1, 1, 0, pl, h, ow)
         wf = weight.as_strided((co, kw * c, kh, 1), (kh * kw * c, 1, kw * c, kw * c))
-        return conv2d(xf, wf, bias, pad=(pt, pb, 0, 0), act=act, wparam=weight)
+        return dict(x=xf, weight=wf, pad=(pt, pb, 0, 0), wparam=weight)
     return None
+
+
+def conv2d_folded(x, weight, bias, stride, pad, act):
+    """conv2d on the tap-folded form (folded_args); None when the shape is not covered."""
+    a = folded_args(x, weight, stride, pad)
+    if a is None:
+        return None
+    return conv2d(bias=bias, act=act, **a)
 
 
 class GradLink(object):
