@@ -223,9 +223,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         const int c = cbase + (((idx & 3) ^ hswz(hp)) * EPC);
         const E* src = Mg + ((mpix[q] >= 0 && c < p.C) ? mpix[q] + c : 0);
         if ((512 * q + 64 * wave) / 4 < hcap)  // wave-uniform; hcap % 16 == 0: the instruction stays inside the buffer
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                           (__attribute__((address_space(3))) void*)(dst + (512 * q + 64 * wave) * 16),
-                                           16, 0, 0);
+          lds_dma16(src, __builtin_amdgcn_readfirstlane(lds_addr(dst + (512 * q + 64 * wave) * 16)));
       }
     }
   };
@@ -245,10 +243,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   auto issue_w = [&](int step, int slot) {
     const char* src = wsrc + (int64_t)step * wstep;
     char* dst = reinterpret_cast<char*>(wts + slot * BNL * 4) + wave * GL * 1024;
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(lds_addr(dst));
 #pragma unroll
-    for (int j = 0; j < GL; ++j)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j * 1024),
-                                       (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, 0, 0);
+    for (int j = 0; j < GL; ++j) lds_dma16(src + j * 1024, d0 + j * 1024);
   };
 
   const int wm = wave / WN, wn = wave % WN;
@@ -567,10 +564,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   X(ID + 5, HL, 208, 8, 1)      \
   X(ID + 6, HL, 192, 4, 2)      \
   X(ID + 7, HL, 80, 8, 1)
+#ifndef TPG_HALO_ISA_ONLY
 #define TPG_HALO_CFGS(X)        \
   TPG_HALO_BN(X, 0, 3)          \
   TPG_HALO_BN(X, 8, 4)          \
   TPG_HALO_BN(X, 16, 5)
+#else  // (ISA inspection builds: the enhance_128 tile only)
+#define TPG_HALO_CFGS(X) X(13, 4, 208, 8, 1)
+#endif
 // 512-row tiles (ids 24, 25): BN 64 / 80 on the large maps, halo up to 1024 pixels
 #define TPG_HALO_CFGS512(X)     \
   X(24, 8, 64, 8, 1)            \
@@ -620,6 +621,13 @@ static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
   return launch_halo_t<DT, HL, BN, WM, WN, MASK, BM, 1>(g, grid, halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3, BM),
                                                         s);
 }
+
+#ifdef TPG_HALO_ISA_ONLY
+#undef TPG_HALO_CFGS512
+#undef TPG_HALO_CFGS_S2
+#define TPG_HALO_CFGS512(X)
+#define TPG_HALO_CFGS_S2(X)
+#endif
 
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask) {
   dim3 grid((a.N * a.tiles_h * a.tiles_w + a.IMG - 1) / a.IMG, a.ntiles, a.ksplit);
@@ -675,6 +683,11 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
   X(40, 8, 32, 8, 1, false)    \
   X(41, 8, 64, 8, 1, false)    \
   X(43, 8, 128, 4, 2, false)
+
+#ifdef TPG_HALO_ISA_ONLY
+#undef TPG_HALO_GROUP_CFGS
+#define TPG_HALO_GROUP_CFGS(X)
+#endif
 
 int launch_halo_group(const HaloArgs* a, int n, int dtype, int cfg, hipStream_t s, bool mask) {
   if (n < 2 || n > TPG_GROUP_MAX || (dtype != 1 && dtype != 2)) return -1;

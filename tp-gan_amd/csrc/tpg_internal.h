@@ -73,6 +73,48 @@ struct FastDiv {
   }
 };
 
+// LDS-DMA of one 16-byte chunk per lane (global_load_lds_dwordx4): lane i's 16 bytes land at
+// LDS byte address lds_base + 16 * i (lds_base wave-uniform).  Inline asm rather than
+// __builtin_amdgcn_global_load_lds: the compiler's wait-count pass treats the builtin's LDS write
+// as an LGKM event of another kind and then waits lgkmcnt(0) before the first MFMA of every
+// pipeline step instead of a counted wait on that step's fragment reads.  Callers order the
+// DMA'd bytes themselves (s_waitcnt vmcnt + s_barrier); the pass, not seeing these loads, only
+// ever waits for more VMEM operations than it needs (in-order completion), never fewer.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_base) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(lds_base));  // (M0 -> LDS-DMA: 1 wait state)
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// s_waitcnt lgkmcnt(n) for an n that is constant once the caller's loops are unrolled (n > 15:
+// the field's maximum, a stricter wait)
+__device__ __forceinline__ void wait_lgkm(int n) {
+  switch (n < 15 ? (n < 0 ? 0 : n) : 15) {
+#define TPG_W(k) case k: asm volatile("s_waitcnt lgkmcnt(" #k ")" ::: "memory"); break;
+    TPG_W(0) TPG_W(1) TPG_W(2) TPG_W(3) TPG_W(4) TPG_W(5) TPG_W(6) TPG_W(7)
+    TPG_W(8) TPG_W(9) TPG_W(10) TPG_W(11) TPG_W(12) TPG_W(13) TPG_W(14) TPG_W(15)
+#undef TPG_W
+  }
+}
+
+// Weight-gradient kernels' first-substep fragment reads (2 transposed reads per fragment; A
+// fragments 0..MREP-1 are reads 0..2*MREP-1, B fragments follow) issued in first-use order of
+// the m-major MFMA sequence: A0, B0 .. B(NREP-1), A1 .. A(MREP-1).  frag_read_order(k) is the
+// read issued k-th; frag_read_wait(i, ...) the lgkmcnt that lets MFMA i start once its own
+// operands have landed, with `later` reads issued after the first substep's.
+template <int MREP, int NREP>
+__device__ __forceinline__ constexpr int frag_read_order(int k) {
+  return k < 2 ? k : k < 2 + 2 * NREP ? 2 * MREP + (k - 2) : 2 + (k - 2 - 2 * NREP);
+}
+template <int MREP, int NREP>
+__device__ __forceinline__ constexpr int frag_read_wait(int i, int later) {
+  constexpr int R = 2 * (MREP + NREP);
+  const int m = i / NREP, n = i % NREP;
+  const int last = m == 0 ? 2 * n + 3 : 2 * NREP + 2 * m + 1;  // position of its last read
+  return R - 1 - last + later;
+}
+
 // Zero the elements of a 16-byte chunk whose channel index (c0 + e) is >= C.
 // Branch-free (selects only) so hipcc keeps loads in flight (no per-element vmcnt(0)).
 template <int EPC>

@@ -266,9 +266,12 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
         return B + row * RBB + (((col >> 3) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 7) * 2;
       };
       s16x4 h[2][R];
+      // (first-use order, counted waits below: the MFMAs start on their own operands)
 #pragma unroll
-      for (int r = 0; r < R; ++r) h[0][r] = tr_read(addr(0, r));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int k = 0; k < R; ++k) {
+        const int r = frag_read_order<MREP, NREP>(k);
+        h[0][r] = tr_read(addr(0, r));
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < NS; ++ks) {
@@ -276,6 +279,10 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           const int m = i / NREP, n = i % NREP;
+          if (ks == 0) {
+            wait_lgkm(frag_read_wait<MREP, NREP>(i, i * R / M));
+            __builtin_amdgcn_sched_barrier(0);
+          }
           const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
                                                                                0, 1, 2, 3, 4, 5, 6, 7));
           const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * n],

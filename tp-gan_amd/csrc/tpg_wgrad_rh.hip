@@ -199,9 +199,12 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       return B + row * RBB + (((cb >> 3) ^ rh_swz<RBB>(row)) << 4) + (cb & 7) * 2;
     };
     s16x4 h[2][R];
+    // (first-use order, counted waits below: the MFMAs start on their own operands)
 #pragma unroll
-    for (int rr = 0; rr < R; ++rr) h[0][rr] = rh_tr_read(addr(0, rr));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int k = 0; k < R; ++k) {
+      const int rr = frag_read_order<MREP, NREP>(k);
+      h[0][rr] = rh_tr_read(addr(0, rr));
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < NS; ++ks) {
@@ -209,6 +212,10 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int m = i / NREP, j = i % NREP;
+        if (ks == 0) {
+          wait_lgkm(frag_read_wait<MREP, NREP>(i, i * R / M));
+          __builtin_amdgcn_sched_barrier(0);
+        }
         const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * m], h[cur][2 * m + 1],
                                                                              0, 1, 2, 3, 4, 5, 6, 7));
         const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * j],
