@@ -63,7 +63,7 @@ def flops(s):
     return 2 * N * OH * OW * Cout * Cin * k * k
 
 
-def run(name, s, iters, passes, sweep=False):
+def run(name, s, iters, passes, sweep=False, wg_algo=0):
     lib = load()
     dev = torch.device("cuda", 0)
     N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
@@ -81,6 +81,8 @@ def run(name, s, iters, passes, sweep=False):
     dx = T.new_act(N, Cin, H, W, dt, dev)
     dw = torch.zeros_like(w)
     d = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
+    wd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
+    wd.algo = wg_algo  # (0: the library's untuned default)
     wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
     wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
     calls = {
@@ -88,7 +90,7 @@ def run(name, s, iters, passes, sweep=False):
                                                 tt(res), tt(y), wsf.data_ptr(), wsf.numel(), stream_ptr())),
         "dgrad": lambda: check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w), tt(dx), wsd.data_ptr(),
                                                        wsd.numel(), stream_ptr())),
-        "wgrad": lambda: check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0,
+        "wgrad": lambda: check(lib.tpg_conv2d_bwd_filter(ctypes.byref(wd), tt(x), tt(g), tt(dw), None, 0,
                                                          stream_ptr())),
     }
     f = flops(s)
@@ -138,11 +140,13 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--wg-sweep", action="store_true", help="time every weight-gradient algo / pixel split")
+    ap.add_argument("--wg-algo", default="", help="weight-gradient algo per shape, e.g. enhance_128=12,add_128=7")
     a = ap.parse_args()
     for name, s in SHAPES.items():
         if a.only and name not in a.only.split(","):
             continue
-        run(name, s, a.iters, a.passes.split(","), a.wg_sweep)
+        algos = dict(kv.split("=") for kv in a.wg_algo.split(",") if kv)
+        run(name, s, a.iters, a.passes.split(","), a.wg_sweep, int(algos.get(name, 0)))
 
 
 if __name__ == "__main__":

@@ -28,6 +28,17 @@
 #include <stdlib.h>
 #include <string.h>
 
+// timing ablations (tools only; never in the product build): bit 1 no weight LDS-DMA, 2 no tap
+// barrier, 4 no MFMA, 8 no fragment reads, 16 no halo loads / stores
+#ifndef TPG_HALO_ABL
+#define TPG_HALO_ABL 0
+#endif
+#if (TPG_HALO_ABL & 2) != 0
+#define HALO_BAR ""
+#else
+#define HALO_BAR "\n\ts_barrier"
+#endif
+
 namespace tpg {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -180,6 +191,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   u32x4 hreg[HL];
   int hc = 0;
   auto load_halo = [&](int ks) {
+    if constexpr ((TPG_HALO_ABL & 16) != 0) return;
     const int cbase = (ks0 + ks) * KS;
     hc = cbase + (tid & 3) * EPC;
 #pragma unroll
@@ -190,6 +202,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   };
   int gch = 0;  // mask mode: channel of this thread's chunks in the last stored halo
   auto store_halo = [&](int buf) {
+    if constexpr ((TPG_HALO_ABL & 16) != 0) return;
     u32x4* H = halo + buf * hcap * 4;
 #pragma unroll
     for (int q = 0; q < HL; ++q) {
@@ -241,6 +254,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   };
   // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
   auto issue_w = [&](int step, int slot) {
+    if constexpr ((TPG_HALO_ABL & 1) != 0) return;
     const char* src = wsrc + (int64_t)step * wstep;
     char* dst = reinterpret_cast<char*>(wts + slot * BNL * 4) + wave * GL * 1024;
     const uint32_t d0 = __builtin_amdgcn_readfirstlane(lds_addr(dst));
@@ -278,7 +292,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll
   for (int n = 0; n < NREP - NH; ++n) hb[n] = u32x4{0u, 0u, 0u, 0u};
   auto mma = [&](u32x4 a, u32x4 b, f32x4 c) -> f32x4 {
-    if constexpr (BF) {
+    if constexpr ((TPG_HALO_ABL & 4) != 0) {
+      c[0] += __builtin_bit_cast(float, a[0] ^ b[1]);
+      return c;
+    } else if constexpr (BF) {
       return mfma16x16x32<DT>(a, b, c);
     } else {
       const f32x4 a4 = __builtin_bit_cast(f32x4, a);
@@ -368,8 +385,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       compute(ks & 1, slot, toff);
       toff = toff_next;
       if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
-      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
       slot = (slot + 1) & 3;
       if (++t == ntaps) { t = 0; ++ks; }
     }
@@ -399,8 +416,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       compute(ks & 1, slot, toff);
       toff = toff_next;
       if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
-      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
       slot = slot == 2 ? 0 : slot + 1;
       if (++t == ntaps) { t = 0; ++ks; }
     }

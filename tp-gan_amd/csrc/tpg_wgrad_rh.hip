@@ -18,6 +18,12 @@
 #include "tpg_internal.h"
 #include <type_traits>
 
+// timing ablations (tools only; never in the product build): bit 1 no LDS-DMA, 2 no barrier,
+// 4 no MFMA, 8 no fragment reads
+#ifndef TPG_RH_ABL
+#define TPG_RH_ABL 0
+#endif
+
 namespace tpg {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -132,6 +138,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   }
 
   auto issue = [&](int slot, int n_, int py_, int px_) {
+    if constexpr ((TPG_RH_ABL & 1) != 0) return;
     char* st = lds + slot * STAGE;
     const int sbase = (n_ * p.p_sn + py_ * p.p_sh + px_ * p.p_sw) * 2;
 #pragma unroll
@@ -203,7 +210,8 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int rr = frag_read_order<MREP, NREP>(k);
-      h[0][rr] = rh_tr_read(addr(0, rr));
+      if constexpr ((TPG_RH_ABL & 8) == 0) h[0][rr] = rh_tr_read(addr(0, rr));
+      else h[0][rr] = s16x4{(short)lane, 1, 2, 3};
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -221,10 +229,14 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * j],
                                                                              h[cur][2 * MREP + 2 * j + 1],
                                                                              0, 1, 2, 3, 4, 5, 6, 7));
-        acc[m][j] = mfma16x16x32<DT>(av, bv, acc[m][j]);
+        if constexpr ((TPG_RH_ABL & 4) == 0) acc[m][j] = mfma16x16x32<DT>(av, bv, acc[m][j]);
+        else acc[m][j][0] += (float)av[0] * (float)bv[1];
         if (ks + 1 < NS) {
 #pragma unroll
-          for (int rr = i * R / M; rr < (i + 1) * R / M; ++rr) h[cur ^ 1][rr] = rh_tr_read(addr(ks + 1, rr));
+          for (int rr = i * R / M; rr < (i + 1) * R / M; ++rr) {
+            if constexpr ((TPG_RH_ABL & 8) == 0) h[cur ^ 1][rr] = rh_tr_read(addr(ks + 1, rr));
+            else h[cur ^ 1][rr] = h[cur][rr];
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -258,6 +270,9 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       if (ix == p.PW) { ix = 0; iy += TH; if (iy >= p.PH) { iy = 0; ++in_; } }  // (partial last band)
     }
   };
+#if (TPG_RH_ABL & 2) != 0
+#define RH_WAIT_BARRIER() asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)" ::: "memory")
+#else
 #define RH_WAIT_BARRIER()                                                                          \
   do {                                                                                             \
     if constexpr (GA + GB == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
@@ -266,6 +281,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
     else if constexpr (GA + GB == 5) asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
     else asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
   } while (0)
+#endif
   static_assert(GA + GB >= 2 && GA + GB <= 6, "vmcnt");
   issue_next(0);
   issue_next(1);
