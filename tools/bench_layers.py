@@ -51,6 +51,12 @@ SHAPES = {
     "dec_img": (32, 32, 128, 128, 3, 3, 1, 1, False, 0, ACT_NONE, False),
     "d_first": (64, 3, 128, 128, 64, 3, 2, 1, False, 0, ACT_LEAKY, False),
     "up_32": (32, 768, 16, 16, 256, 3, 2, 1, True, 1, ACT_RELU, False),
+    # tiny layers (D_and_G_model.py:212 fc1, :220 deconv_32, :222 deconv_128, :81 local_img)
+    "fc1": (32, 32768, 1, 1, 512, 1, 1, 0, False, 0, ACT_NONE, False),
+    "deconv_32": (32, 64, 8, 8, 32, 3, 4, 0, True, 1, ACT_RELU, False),
+    "deconv_128": (32, 16, 64, 64, 8, 3, 2, 1, True, 1, ACT_RELU, False),
+    "local_img": (32, 64, 40, 40, 3, 1, 1, 0, False, 0, ACT_NONE, False),
+    "local_fold": (32, 27, 40, 40, 64, 1, 1, 0, False, 0, ACT_LEAKY, False),
 }
 
 

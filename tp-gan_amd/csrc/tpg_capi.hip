@@ -368,11 +368,15 @@ static std::vector<Prob> subpixel_probs(int OH, int OW, int kh, int kw, int sh, 
 }
 
 // stride 2 on maps of <= 64 x 64 outputs (A/B hooks TPG_NO_DILATED, TPG_DILATED_MAXPIX; 64x64: conv2
-// s2 dgrad 0.096 -> 0.039 ms, step -0.3 ms)
+// s2 dgrad 0.096 -> 0.039 ms, step -0.3 ms); stride 4 likewise (deconv_32, D_and_G_model.py:220:
+// sixteen parity classes, four of them without a tap: 0.138 -> 0.023 ms).  (Thin layers on
+// larger maps stay in class form: deconv_128, 16 -> 8 channels at 128x128, measured 54 -> 63 us
+// in the zero-insertion form.)
 static bool use_dilated(int OH, int OW, int kh, int kw, int sh, int sw, int pad_mode) {
   static const bool off = getenv("TPG_NO_DILATED") != nullptr;
   static const int maxpix = getenv("TPG_DILATED_MAXPIX") ? atoi(getenv("TPG_DILATED_MAXPIX")) : 64 * 64;
-  return !off && sh == 2 && sw == 2 && pad_mode == TPG_PAD_ZERO && kh <= 5 && kw <= 5 && OH * OW <= maxpix;
+  return !off && sh == sw && (sh == 2 || sh == 4) && pad_mode == TPG_PAD_ZERO && kh <= 5 && kw <= 5 &&
+         OH * OW <= maxpix;
 }
 
 // zero-insertion form of the same problem (stride-2, small maps): ONE unit-stride problem

@@ -589,7 +589,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #else  // (ISA inspection builds: the enhance_128 tile only)
 #define TPG_HALO_CFGS(X) X(13, 4, 208, 8, 1)
 #endif
-// 512-row tiles (ids 24, 25): BN 64 / 80 on the large maps, halo up to 1024 pixels
+// 512-row tiles (ids 24, 25): BN 64 / 80 on the large maps, halo up to 1024 pixels (a BN-32
+// variant for decoded_img128, D_and_G_model.py:279, measured slower: 47 -> 61 us forward)
 #define TPG_HALO_CFGS512(X)     \
   X(24, 8, 64, 8, 1)            \
   X(25, 8, 80, 8, 1)
