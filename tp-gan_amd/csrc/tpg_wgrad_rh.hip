@@ -37,12 +37,15 @@ __device__ __forceinline__ s16x4 rh_tr_read(const char* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
   return v;
 }
-// the same read as a builtin: the compiler sees an LDS load, so a constant part of the address
-// goes into the instruction's offset field (and its own lgkmcnt waits match the counted ones)
-__device__ __forceinline__ s16x4 rh_tr_read_c(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) char*)p);
+// with a constant part of the address in the instruction's offset field (off: a constant once
+// the caller's loops are unrolled)
+__device__ __forceinline__ s16x4 rh_tr_read_o(const char* base, int off) {
+  s16x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)base;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(off));
+  return v;
 }
+
 
 // chunk swizzles of the LDS rows (256- and 128-byte rows as in tpg_wgrad2.hip; 64-byte rows:
 // the g = 0 / 1 row octets of a transposed read use disjoint chunk pairs)
@@ -186,10 +189,8 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   // Row mode: per-lane LDS byte offsets of the fragment reads.  The chunk swizzles depend on
   // the row only through bits the substep (+32 rows) and, for A, the K half (+4 rows) leave
   // alone, so every read is one of MREP + 2 * NREP lane offsets plus a constant (the
-  // instruction's offset field, builtin reads): ~40 % fewer VALU in the k-tile loop.
-  // (measured per tile: 128 x 32 / 64 x 64 -11 %, 256 x 32 +18 % -- the latter keeps the asm
-  // reads of per-read addresses)
-  constexpr bool IMM = NR == 1 && BM <= 128;
+  // instruction's offset field): ~40 % fewer VALU in the k-tile loop.
+  constexpr bool IMM = NR == 1;
   int abase[IMM ? MREP : 1], bbase[IMM ? NREP : 1][2];
   if constexpr (IMM) {
 #pragma unroll
@@ -224,11 +225,6 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
     constexpr int NS = KP / 32;
     constexpr int R = 2 * (MREP + NREP), M = MREP * NREP;
     auto addr = [&](int ks, int rr) -> const char* {
-      if constexpr (IMM) {
-        if (rr < 2 * MREP) return A + abase[rr >> 1] + (32 * ks + 4 * (rr & 1)) * RBA;
-        const int r2 = rr - 2 * MREP;
-        return A + bbase[r2 >> 1][r2 & 1] + 32 * ks * RBB;
-      }
       if (rr < 2 * MREP) {
         const int col = wm * WTM + (rr >> 1) * 16 + 4 * p4;
         const int row = ks * 32 + 8 * g + 4 * (rr & 1) + q;
@@ -240,12 +236,23 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
       const int row = kbase[ks][r2 & 1] + (tap / NT) * HW + tap % NT;
       return B + row * RBB + (((cb >> 3) ^ rh_swz<RBB>(row)) << 4) + (cb & 7) * 2;
     };
+    // IMM: lane base + constant offset (asm: a builtin LDS read makes hipcc put vmcnt(0) in
+    // front of it for the in-flight LDS-DMA, measured +18 % on the 256 x 32 tile)
+    auto rd = [&](int ks, int rr) -> s16x4 {
+      if constexpr (IMM) {
+        if (rr < 2 * MREP) return rh_tr_read_o(A + abase[rr >> 1], (32 * ks + 4 * (rr & 1)) * RBA);
+        const int r2 = rr - 2 * MREP;
+        return rh_tr_read_o(A + bbase[r2 >> 1][r2 & 1], 32 * ks * RBB);
+      } else {
+        return rh_tr_read(addr(ks, rr));
+      }
+    };
     s16x4 h[2][R];
     // (first-use order, counted waits below: the MFMAs start on their own operands)
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int rr = frag_read_order<MREP, NREP>(k);
-      if constexpr ((TPG_RH_ABL & 8) == 0) h[0][rr] = IMM ? rh_tr_read_c(addr(0, rr)) : rh_tr_read(addr(0, rr));
+      if constexpr ((TPG_RH_ABL & 8) == 0) h[0][rr] = rd(0, rr);
       else h[0][rr] = s16x4{(short)lane, 1, 2, 3};
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
 #pragma unroll
           for (int rr = i * R / M; rr < (i + 1) * R / M; ++rr) {
             if constexpr ((TPG_RH_ABL & 8) == 0)
-              h[cur ^ 1][rr] = IMM ? rh_tr_read_c(addr(ks + 1, rr)) : rh_tr_read(addr(ks + 1, rr));
+              h[cur ^ 1][rr] = rd(ks + 1, rr);
             else h[cur ^ 1][rr] = h[cur][rr];
           }
         }
