@@ -30,11 +30,12 @@ __device__ __forceinline__ int w2_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-// ds_read_b64_tr_b16 through inline asm (see compute())
-__device__ __forceinline__ s16x4 tr_read(const char* p) {
+// ds_read_b64_tr_b16 through inline asm (see compute()) at base + off, off in the
+// instruction's offset field (a constant once the caller's loops are unrolled)
+__device__ __forceinline__ s16x4 tr_read_o(const char* base, int off) {
   s16x4 v;
-  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)base;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(off));
   return v;
 }
 
@@ -238,6 +239,21 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4r{one_pair<DT>(), one_pair<DT>(), one_pair<DT>(), one_pair<DT>()});
+  // per-lane LDS byte offsets of the 16-bit fragment reads (see rd in compute)
+  int abase[BF ? MREP : 1], bbase[BF ? NREP : 1];
+  if constexpr (BF) {
+    const int q = l16 >> 2, p4 = l16 & 3, row = 8 * g + q;
+#pragma unroll
+    for (int m = 0; m < MREP; ++m) {
+      const int col = wm * WTM + m * 16 + 4 * p4;
+      abase[m] = row * RBA + (((col >> 3) ^ w2_swz<BF, RBA>(row)) << 4) + (col & 7) * 2;
+    }
+#pragma unroll
+    for (int n = 0; n < NREP; ++n) {
+      const int col = wn * WTN + n * 16 + 4 * p4;
+      bbase[n] = row * RBB + (((col >> 3) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 7) * 2;
+    }
+  }
 
   // BIAS (compile-time): also the bias MFMAs, right beside the regular MFMA that already
   // holds each A fragment (a runtime branch inside this hand-scheduled region let the compiler
@@ -253,24 +269,20 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
       // and the ISA is checked to hold them in place (no copies before the wait).
       constexpr int NS = KP / 32;
       constexpr int R = 2 * (MREP + NREP), M = MREP * NREP;
-      const int q = l16 >> 2, p4 = l16 & 3;
-      auto addr = [&](int ks, int r) -> const char* {
-        if (r < 2 * MREP) {
-          const int col = wm * WTM + (r >> 1) * 16 + 4 * p4;
-          const int row = ks * 32 + 8 * g + 4 * (r & 1) + q;
-          return A + row * RBA + (((col >> 3) ^ w2_swz<BF, RBA>(row)) << 4) + (col & 7) * 2;
-        }
+      // read r of substep ks: row ks*32 + 8g + 4(r & 1) + q, whose swizzle depends on the lane
+      // alone (bits 0-1 and 3 of the row), so a per-lane base of each fragment plus a constant
+      // (lane bases: abase / bbase, computed once per block)
+      auto rd = [&](int ks, int r) -> s16x4 {
+        if (r < 2 * MREP) return tr_read_o(A + abase[r >> 1], (32 * ks + 4 * (r & 1)) * RBA);
         const int rr = r - 2 * MREP;
-        const int col = wn * WTN + (rr >> 1) * 16 + 4 * p4;
-        const int row = ks * 32 + 8 * g + 4 * (rr & 1) + q;
-        return B + row * RBB + (((col >> 3) ^ w2_swz<BF, RBB>(row)) << 4) + (col & 7) * 2;
+        return tr_read_o(B + bbase[rr >> 1], (32 * ks + 4 * (rr & 1)) * RBB);
       };
       s16x4 h[2][R];
       // (first-use order, counted waits below: the MFMAs start on their own operands)
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int r = frag_read_order<MREP, NREP>(k);
-        h[0][r] = tr_read(addr(0, r));
+        h[0][r] = rd(0, r);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -291,7 +303,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
           acc[m][n] = mfma16x16x32<DT>(av, bv, acc[m][n]);
           if (ks + 1 < NS) {
 #pragma unroll
-            for (int r = i * R / M; r < (i + 1) * R / M; ++r) h[cur ^ 1][r] = tr_read(addr(ks + 1, r));
+            for (int r = i * R / M; r < (i + 1) * R / M; ++r) h[cur ^ 1][r] = rd(ks + 1, r);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
