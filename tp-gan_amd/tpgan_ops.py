@@ -143,8 +143,16 @@ def side_streams(device, n, tag=""):
     be in flight at the same time ask with different tags)."""
     key = (torch.device(device).index, n, tag)
     if key not in _SIDE:
-        _SIDE[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+        prio = SIDE_PRIORITY.get(tag, 0)
+        _SIDE[key] = [torch.cuda.Stream(device=device, priority=prio) for _ in range(n)]
     return _SIDE[key]
+
+
+# HIP stream priorities of the side streams (lower = higher priority).  The local pathways'
+# backward runs beside the global pathway's and, sharing the CUs with it, used to finish ~1 ms
+# after it (the G Adam waited for it: profiles/r03 stream split); at high priority their
+# workgroups are dispatched first and the global chain fills the rest of the chip.
+SIDE_PRIORITY = {"local": int(os.environ.get("TPG_LOCAL_PRIORITY", "0"))}
 
 
 _ROCTX = [None]
