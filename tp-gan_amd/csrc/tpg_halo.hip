@@ -253,11 +253,15 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     }
   };
   // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
+  // (the ring's LDS address and the step offset as 32-bit scalars: the generic-pointer form
+  // cost a 64-bit multiply, an address-space null check and two readfirstlanes per step)
+  const uint32_t wts_lds = __builtin_amdgcn_readfirstlane(lds_addr(wts)) +
+                           (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (GL * 1024);
+  const uint32_t wstep32 = (uint32_t)wstep;  // (packed image < 2^31 bytes: planner)
   auto issue_w = [&](int step, int slot) {
     if constexpr ((TPG_HALO_ABL & 1) != 0) return;
-    const char* src = wsrc + (int64_t)step * wstep;
-    char* dst = reinterpret_cast<char*>(wts + slot * BNL * 4) + wave * GL * 1024;
-    const uint32_t d0 = __builtin_amdgcn_readfirstlane(lds_addr(dst));
+    const char* src = wsrc + (uint32_t)step * wstep32;
+    const uint32_t d0 = wts_lds + (uint32_t)slot * (BNL * 64);
 #pragma unroll
     for (int j = 0; j < GL; ++j) lds_dma16(src + j * 1024, d0 + j * 1024);
   };
