@@ -267,7 +267,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   };
 
   const int wm = wave / WN, wn = wave % WN;
-  const int l16 = lane & 15, g = lane >> 4;
+  const int l16 = lane & 15, g = lane >> 4, g16 = g << 4;
   int hbase[MREP];
 #pragma unroll
   for (int m = 0; m < MREP; ++m) {
@@ -287,7 +287,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   // (operands held in registers, +28 VGPRs) and issue them first in the next step, so each
   // SIMD has matrix work while its partner wave waits for the step's fragment reads
   // (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Measured ~1 % on the 128x128 layers.
+  // (off since round 3: with the leaner step body the carried MFMAs' register copies cost
+  // more than the overlap gave -- dgrad enhance_128 1.115 -> 1.081 ms, step 35.71 -> 35.63 ms
+  // same box; -DTPG_HALO_LAG builds it back in)
+#ifdef TPG_HALO_LAG
   constexpr bool LAG_OK = BF && BN >= 128;
+#else
+  constexpr bool LAG_OK = false;
+#endif
   constexpr int NH = LAG_OK ? (NREP + 1) / 2 : NREP;
   const bool lag = LAG_OK && !(p.var & 8) && wave >= 4;
   u32x4 ha[MREP], hb[NREP - NH + 1];
@@ -323,8 +330,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     u32x4 af[MREP];
 #pragma unroll
     for (int m = 0; m < MREP; ++m) {
+      // byte offset hp * 64 + 16 * (g ^ hswz(hp)) = (hp << 6) + ((g << 4) ^ ((hp << 3) & 32))
       const int hp = hbase[m] + toff;
-      af[m] = H[hp * 4 + (g ^ hswz(hp))];
+      af[m] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(H) + (hp << 6) + (g16 ^ ((hp << 3) & 32)));
     }
     // all B fragments of the step are read up front into their own registers: reusing one
     // register quad across n made hipcc wait (lgkmcnt(0)) before every B read, exposing
