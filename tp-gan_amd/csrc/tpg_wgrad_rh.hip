@@ -207,6 +207,15 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         const int row = 8 * g + 4 * h + q + tap;  // (row mode: halo row = pixel + tap)
         bbase[j][h] = BYTES_A + row * RBB + (((cb >> 3) ^ rh_swz<RBB>(row)) << 4) + (cb & 7) * 2;
       }
+    // opaque to the optimiser: kept as one register each (rematerialised from their parts they
+    // cost two VALU per read and k-tile)
+#pragma unroll
+    for (int m = 0; m < MREP; ++m) asm volatile("" : "+v"(abase[m]));
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      asm volatile("" : "+v"(bbase[j][0]));
+      asm volatile("" : "+v"(bbase[j][1]));
+    }
   }
   // halo row of this lane's pixel k = ks*32 + 8g + 4h + q for tap (0, 0): (k / TW) * HW + k % TW
   int kbase[2][2];
