@@ -110,6 +110,12 @@ def test_bad_descriptors(lib):
     d.pad_mode = L.PAD_REFLECT
     assert lib.tpg_conv2d_workspace(ctypes.byref(d), L.OP_FWD) == 0
     assert b"reflect" in lib.tpg_last_error()
+    # a kernel larger than the padded input: C's truncating division gives a "consistent"
+    # 0- or 1-pixel output that torch rejects (the 0-pixel case divided by zero in the planner)
+    for k, s in ((3, 2), (3, 3)):
+        d = _desc(2, 16, 1, 1, 16, k, s, 0)
+        assert lib.tpg_conv2d_workspace(ctypes.byref(d), L.OP_FWD) == 0
+        assert b"larger than the padded input" in lib.tpg_last_error() or b"empty" in lib.tpg_last_error()
 
 
 def test_null_tensor_rejected_without_device_work(lib):
@@ -117,3 +123,24 @@ def test_null_tensor_rejected_without_device_work(lib):
     z = L.TpgTensor()
     rc = lib.tpg_conv2d_fwd(ctypes.byref(d), z, z, None, z, z, None, 0, None)
     assert rc < 0 and b"NULL" in lib.tpg_last_error()
+
+
+def test_planner_sanitizer_sweep():
+    """The planner (descriptor validation, plans, workspace and pre-pack sizing) rebuilt with
+    host AddressSanitizer + UBSan and driven over TP-GAN's layer shapes, a seeded random walk of
+    geometries and malformed descriptors (tools/planner_asan.cpp).  The sweep first found a
+    divide-by-zero on a 0-pixel Conv2d output, now rejected by check_desc."""
+    import shutil
+    import subprocess
+    src = os.path.join(REPO, "tp-gan_amd")
+    objs = [os.path.join(src, "build", f) for f in os.listdir(os.path.join(src, "build"))
+            if f.endswith(".o")] if os.path.isdir(os.path.join(src, "build")) else []
+    if not shutil.which("/opt/rocm/bin/hipcc") or len(objs) < 8:
+        pytest.skip("needs hipcc and the built kernel objects (make -C tp-gan_amd)")
+    r = subprocess.run(["make", "-s", "-C", src, "asan"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([os.path.join(src, "build", "asan", "planner_asan"), "20000"], capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "ok" in r.stdout and "ERROR" not in r.stderr, r.stdout + r.stderr[-4000:]

@@ -428,6 +428,11 @@ static int32_t check_desc(const tpg_conv_desc* d) {
   if (!d) return fail(-1, "null descriptor");
   if (d->n <= 0 || d->in_c <= 0 || d->out_c <= 0 || d->kh <= 0 || d->kw <= 0) return fail(-2, "bad sizes");
   if (d->stride_h <= 0 || d->stride_w <= 0) return fail(-2, "bad stride");
+  // empty maps, and (Conv2d) a kernel larger than the padded input, which C's truncating
+  // division would otherwise turn into a 0- or 1-pixel output (torch rejects both)
+  if (d->in_h <= 0 || d->in_w <= 0 || d->out_h <= 0 || d->out_w <= 0) return fail(-2, "empty spatial map");
+  if (!d->transposed && (d->in_h + d->pad_t + d->pad_b < d->kh || d->in_w + d->pad_l + d->pad_r < d->kw))
+    return fail(-6, "kernel %dx%d larger than the padded input", d->kh, d->kw);
   if (d->dtype != TPG_F32 && d->dtype != TPG_BF16 && d->dtype != TPG_F16) return fail(-3, "bad dtype %d", d->dtype);
   // more taps than the tap tables hold: only the full-kernel GEMM forms (fc1 / deconv_8 at
   // 256x256: 16x16 kernels on a 16x16 map or from a 1x1 map), which need no tap table
