@@ -69,7 +69,33 @@ def flops(s):
     return 2 * N * OH * OW * Cout * Cin * k * k
 
 
-def run(name, s, iters, passes, sweep=False, wg_algo=0):
+def timed(fn, iters, graph):
+    """ms per call of fn over iters back-to-back calls.  graph: the calls are captured into one
+    HIP graph and replayed, so the time is the GPU's alone (eagerly, ctypes issue of a short
+    kernel -- ~20 us -- outruns the kernel and the loop measures the host)."""
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if graph:
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(iters):
+                fn()
+        gr.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        gr.replay()
+        e1.record()
+    else:
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False):
     lib = load()
     dev = torch.device("cuda", 0)
     N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
@@ -108,14 +134,9 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0):
                 rc = lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0, stream_ptr())
                 if rc:
                     break
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(iters):
-                    lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0, stream_ptr())
-                e1.record()
-                torch.cuda.synchronize()
-                res.append((e0.elapsed_time(e1) / iters, algo, ks))
+                ms = timed(lambda: lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0,
+                                                              stream_ptr()), iters, graph)
+                res.append((ms, algo, ks))
         d.algo, d.ksplit = 0, 0
         res.sort()
         print("%-12s wgrad sweep best: %s" % (name, "  ".join("a%d/k%d %.3f ms %.0f TF/s" % (a_, k_, ms, f / ms / 1e9)
@@ -127,14 +148,7 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0):
             continue
         for _ in range(3):
             fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / iters
+        ms = timed(fn, iters, graph)
         tf = f / (ms * 1e-3) / 1e12
         out.append("%s %.3f ms %.0f TF/s (%.1f%%)" % (kind, ms, tf, 100 * tf / 2500))
     print("%-12s %6.1f GF | %s" % (name, f / 1e9, " | ".join(out)), flush=True)
@@ -147,12 +161,13 @@ def main():
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--wg-sweep", action="store_true", help="time every weight-gradient algo / pixel split")
     ap.add_argument("--wg-algo", default="", help="weight-gradient algo per shape, e.g. enhance_128=12,add_128=7")
+    ap.add_argument("--graph", action="store_true", help="time graph replays (GPU time of short kernels)")
     a = ap.parse_args()
     for name, s in SHAPES.items():
         if a.only and name not in a.only.split(","):
             continue
         algos = dict(kv.split("=") for kv in a.wg_algo.split(",") if kv)
-        run(name, s, a.iters, a.passes.split(","), a.wg_sweep, int(algos.get(name, 0)))
+        run(name, s, a.iters, a.passes.split(","), a.wg_sweep, int(algos.get(name, 0)), a.graph)
 
 
 if __name__ == "__main__":

@@ -50,6 +50,15 @@ __device__ __forceinline__ int w2_swz(int row) {
   }
 }
 
+// Ring depth: TPG_W2_NST stages (default 3: two k-tiles in flight) where NST stages of the tile
+// fit in half the CU's LDS (two blocks per CU), else 3.
+#ifndef TPG_W2_NST
+#define TPG_W2_NST 3
+#endif
+__host__ __device__ constexpr int w2_stages(int dt, int bm, int bn) {
+  return (TPG_W2_NST * (dt ? 64 * (bm + bn) * 2 : 32 * (bm + bn) * 4) <= 80 * 1024) ? TPG_W2_NST : 3;
+}
+
 template <int DT, int BM, int BN, int WM, int WN, bool FLAT, int NG = 1>
 __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, NG> G) {
   // grouped launch: member m owns blocks [boff[m], boff[m + 1]) (its own 1-D grid)
@@ -70,12 +79,14 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
   constexpr int BYTES_A = KP * RBA, BYTES_B = KP * RBB;
   constexpr int GA = BYTES_A / 8192, GB = BYTES_B / 8192;  // 1 KiB DMA pieces per wave
   constexpr int STAGE = BYTES_A + BYTES_B;
+  constexpr int NST = w2_stages(DT, BM, BN);  // LDS ring depth: NST-1 k-tiles in flight
+  static_assert((NST - 2) * (GA + GB) <= 63, "vmcnt field");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MREP = WTM / 16, NREP = WTN / 16;
   static_assert(GA * 8192 == BYTES_A && GB * 8192 == BYTES_B && GA >= 1 && GB >= 1, "tile bytes");
   static_assert(WM * WN == 8 && MREP * 16 * WM == BM && NREP * 16 * WN == BN, "waves");
 
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [3][STAGE]
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [NST][STAGE]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // 1-D grid, logical block = (tile, tap, split), tile fastest.  Physical block b runs on
   // XCD b % 8; each XCD is handed a contiguous range of logical blocks, so the tiles that
@@ -354,26 +365,21 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
     }
   };
 
-#define W2_WAIT_BARRIER()                                                                          \
-  do {                                                                                             \
-    if constexpr (GA + GB == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
-    else if constexpr (GA + GB == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
-    else if constexpr (GA + GB == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
-    else if constexpr (GA + GB == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
-  } while (0)
+// k-tile kt+1 retired, the NST-2 k-tiles after it still in flight
+#define W2_WAIT_BARRIER() \
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"((NST - 2) * (GA + GB)) : "memory")
 
   if (nkt > 0) {
-    issue(0, 0);
-    issue(min(1, nkt - 1), 1);
+#pragma unroll
+    for (int j = 0; j < NST - 1; ++j) issue(min(j, nkt - 1), j);
     W2_WAIT_BARRIER();  // retires k-tile 0
     int slot = 0;
     for (int kt = 0; kt < nkt; ++kt) {
-      const int slot2 = slot == 0 ? 2 : slot - 1;
-      issue(min(kt + 2, nkt - 1), slot2);  // unconditional (clamped): static vmcnt
+      const int slot2 = slot == 0 ? NST - 1 : slot - 1;
+      issue(min(kt + NST - 1, nkt - 1), slot2);  // unconditional (clamped): static vmcnt
       compute(slot, bias_wave && (kt_base + kt) % p.bshare == sid);  // (one inlined copy)
-      W2_WAIT_BARRIER();                   // retires k-tile kt+1, kt+2 stays in flight
-      slot = slot == 2 ? 0 : slot + 1;
+      W2_WAIT_BARRIER();
+      slot = slot == NST - 1 ? 0 : slot + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -446,7 +452,7 @@ static int w2_blocks(const Wgrad2Args& a, int bm, int bn) {
 template <int DT, int BM, int BN, int WM, int WN, bool FLAT, int NG>
 static int launch_w2_k(const Grouped<Wgrad2Args, NG>& g, int blocks, hipStream_t s) {
   auto k = wgrad2_kernel<DT, BM, BN, WM, WN, FLAT, NG>;
-  const size_t lds = 3 * (DT ? 64 * (BM + BN) * 2 : 32 * (BM + BN) * 4);
+  const size_t lds = w2_stages(DT, BM, BN) * (DT ? 64 * (BM + BN) * 2 : 32 * (BM + BN) * 4);
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                       true);
   (void)once;

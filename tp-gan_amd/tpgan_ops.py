@@ -314,6 +314,61 @@ def _wgrad_key(d):
     return ("wgrad", _desc_tuple(d) + (int(d.flags & FLAG_CONCURRENT),))
 
 
+_TUNE_GRAPH = os.environ.get("TPG_TUNE_GRAPH", "1") != "0"
+_TUNE_REPS = 4
+_TUNE_STREAMS = {}
+
+
+def _tune_stream():
+    dev = torch.cuda.current_device()
+    s = _TUNE_STREAMS.get(dev)
+    if s is None:
+        s = _TUNE_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def _time_wgrad(lib, d, x, g, scratch):
+    """GPU times (ms) of one tpg_conv2d_bwd_filter candidate.  Default: _TUNE_REPS launches
+    captured into one HIP graph, replayed twice, the second replay timed -- the GPU's time
+    alone.  (Eager event pairs around one launch also time the host's ~20 us ctypes issue of
+    the launch, comparable to a small layer's whole weight gradient, so candidates a few us
+    apart were ranked by host jitter; TPG_TUNE_GRAPH=0 restores that timing for A/B.)"""
+    if not _TUNE_GRAPH:
+        ms = []
+        for rep in range(2):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(scratch), None, 0, stream_ptr()))
+            e1.record()
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        return ms
+    # (capture_begin on a stream of our own rather than torch.cuda.graph(), whose entry runs
+    # gc.collect() + empty_cache() -- thousands of trials; thread-local capture: the tuner
+    # runs on autograd's device thread)
+    gr = torch.cuda.CUDAGraph()
+    cs = _tune_stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        gr.capture_begin(capture_error_mode="thread_local")
+        try:
+            for _ in range(_TUNE_REPS):
+                check(lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(scratch), None, 0, stream_ptr()))
+        finally:
+            gr.capture_end()
+    gr.replay()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    gr.replay()
+    e1.record()
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / _TUNE_REPS
+    del gr
+    return [t]
+
+
 def _tuned_wgrad(lib, d, x, g, dwv):
     """(algo, ksplit) for this weight-gradient shape, tuning it on first use (pixel splits
     capped at 16 for ops planned for a share of the chip)."""
@@ -333,19 +388,11 @@ def _tuned_wgrad(lib, d, x, g, dwv):
             if ks > nkt or (ks > 16 and (d.flags & FLAG_CONCURRENT)):
                 break
             d.algo, d.ksplit = algo, ks
-            ms = []
-            for rep in range(3):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-                rc = lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(scratch), None, 0, stream_ptr())
-                e1.record()
-                if rc == -30:  # algos 6..12 (row / image-halo kernel) do not cover this shape
-                    break
-                check(rc)
-                e1.synchronize()
-                if rep:
-                    ms.append(e0.elapsed_time(e1))
+            rc = lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(scratch), None, 0, stream_ptr())
+            if rc == -30:  # algos 6..12 (row / image-halo kernel) do not cover this shape
+                break
+            check(rc)
+            ms = _time_wgrad(lib, d, x, g, scratch)
             AUTOTUNE["trials"] += 1
             if not ms:
                 break
