@@ -58,13 +58,16 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--graph", action="store_true",
-                    help="replay the step as hipGraph(s); off by default: on ROCm 7 the captured graph runs the "
-                         "local-pathway side-stream branches serially (54.6 vs 47.1 ms/step measured)")
+                    help="replay the step as hipGraph(s) with packet capture off and 8 graph queues, so the "
+                         "side-stream branches stay concurrent (37.0 ms/step, no faster than eager: DESIGN.md §4)")
     ap.add_argument("--segmented", action="store_true", help="one hipGraph per step phase even at world 1")
     ap.add_argument("--probe-steps", type=int, default=2)
     ap.add_argument("--identity", choices=["none", "resnet50", "mobilenetv2"], default=None,
                     help="identity-preserving loss extractor in the G step (BASELINE configs[2]: resnet50)")
     ap.add_argument("--gp", action="store_true", help="WGAN-GP in the D step (double backward through D)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI, the product; gloo: the "
+                         "one-GPU rehearsal of this launch path in tests/test_gpu_bench_dp.py)")
     a = ap.parse_args()
     dflt = {2: (32, 128, "bf16", "none"), 3: (32, 128, "bf16", "resnet50"), 5: (16, 256, "fp16", "mobilenetv2")}
     b, im, dt, ident = dflt[a.config]
@@ -80,10 +83,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible devices share them (the gloo rehearsal of
+    # this path runs two ranks on one GPU -- RCCL itself needs a device per rank)
+    # (device_count does not initialise HIP: nothing GPU-side happens before the process group)
+    ndev = max(torch.cuda.device_count(), 1)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     torch.manual_seed(1234)
 
     import D_and_G_model as DG
@@ -255,6 +265,12 @@ def main():
                       "frac_of_peak": round(flops_step / (ms_per_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)},
         "cpu_baseline": cpu,
     }
+    if world > 1:
+        out["dp"] = {"backend": args.dist_backend, "devices": ndev,
+                     "real_ahead_reused": trainer.real_ahead_used,
+                     "g_buckets": len(trainer.gsync.buckets) if trainer.gsync is not None else 0,
+                     "d_buckets": len(trainer.dsync.buckets) if trainer.dsync is not None else 0,
+                     "bucket_order_learned": bool(trainer.gsync is not None and trainer.gsync.order_learned)}
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,49 @@
+"""GPU: bench.py's own data-parallel launch path, rehearsed on ONE device.
+
+The driver's 8-GPU scaling run launches `python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N ...` over RCCL; this test runs that same command line with 2 processes that
+share cuda:0 over gloo (`--dist-backend gloo`: RCCL needs one device per rank), so the env
+parsing, process-group init, device mapping, barrier + max-over-ranks timing, bucketed
+overlapped all-reduces and the real_ahead D(real) pass have executed before the
+driver's run.  The launcher is a child process started by this one (nothing re-execs).
+Reference: single-device `Pretrain.py:111`."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(400)
+def test_bench_torchrun_two_ranks_one_gpu(gpu):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "2", "--batch", "2", "--no-cpu-baseline",
+           "--dist-backend", "gloo"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=380)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # rank 0 alone prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["scaling"] == "weak"
+    assert out["config"]["global_batch"] == 4 and out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    dp = out["dp"]
+    assert dp["backend"] == "gloo"
+    # every step after the first reuses the D(real) pass the previous one ran under G's tail
+    assert dp["real_ahead_reused"] >= 2, dp
+    assert dp["g_buckets"] > 1 and dp["d_buckets"] >= 1 and dp["bucket_order_learned"], dp

@@ -284,12 +284,18 @@ class Generator(nn.Module):
                                             img_size=img_size)
         self.local_fuser = LocalFuser(img_size)
         self.feature_predict = FeaturePredict(num_classes)
+        self._groupable = None
 
     def forward(self, I128, left_eye, right_eye, nose, mouth, z, use_dropout):
         paths = (self.local_pathway_left_eye, self.local_pathway_right_eye, self.local_pathway_nose,
                  self.local_pathway_mouth)
         patches = (left_eye, right_eye, nose, mouth)
-        if tpgan_ops.GROUP["enabled"] and I128.is_cuda:
+        if self._groupable is None:
+            # lockstep grouping fuses conv + bias + activation layers only: with BatchNorm
+            # (use_batchnorm=True, the reference default) group_forward would run the members
+            # one by one on one stream, so those pathways keep one stream each instead
+            self._groupable = not any(isinstance(m, nn.BatchNorm2d) for p in paths for m in p.modules())
+        if tpgan_ops.GROUP["enabled"] and I128.is_cuda and self._groupable:
             # the four local pathways in lockstep on one side stream (one grouped launch per
             # layer and kernel), concurrently with the global pathway's local-independent part
             main = torch.cuda.current_stream()

@@ -52,9 +52,8 @@ static thread_local int g_share = 1;
 struct ShareScope {
   int prev;
   explicit ShareScope(const tpg_conv_desc* d) : prev(g_share) {
-    // share of the chip a concurrent op plans for (1 / share); TPG_CONCURRENT_SHARE: A/B hook
-    static const int share = getenv("TPG_CONCURRENT_SHARE") ? std::max(1, atoi(getenv("TPG_CONCURRENT_SHARE"))) : 4;
-    g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? share : 1;
+    // (1/2 .. 1/8 measured within run-to-run spread, profiles/r02c/share)
+    g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? 4 : 1;
   }
   ~ShareScope() { g_share = prev; }
 };
@@ -367,16 +366,14 @@ static std::vector<Prob> subpixel_probs(int OH, int OW, int kh, int kw, int sh, 
   return v;
 }
 
-// stride 2 on maps of <= 64 x 64 outputs (A/B hooks TPG_NO_DILATED, TPG_DILATED_MAXPIX; 64x64: conv2
+// stride 2 on maps of <= 64 x 64 outputs (64x64: conv2
 // s2 dgrad 0.096 -> 0.039 ms, step -0.3 ms); stride 4 likewise (deconv_32, D_and_G_model.py:220:
 // sixteen parity classes, four of them without a tap: 0.138 -> 0.023 ms).  (Thin layers on
 // larger maps stay in class form: deconv_128, 16 -> 8 channels at 128x128, measured 54 -> 63 us
 // in the zero-insertion form.)
 static bool use_dilated(int OH, int OW, int kh, int kw, int sh, int sw, int pad_mode) {
-  static const bool off = getenv("TPG_NO_DILATED") != nullptr;
-  static const int maxpix = getenv("TPG_DILATED_MAXPIX") ? atoi(getenv("TPG_DILATED_MAXPIX")) : 64 * 64;
-  return !off && sh == sw && (sh == 2 || sh == 4) && pad_mode == TPG_PAD_ZERO && kh <= 5 && kw <= 5 &&
-         OH * OW <= maxpix;
+  return sh == sw && (sh == 2 || sh == 4) && pad_mode == TPG_PAD_ZERO && kh <= 5 && kw <= 5 &&
+         OH * OW <= 64 * 64;
 }
 
 // zero-insertion form of the same problem (stride-2, small maps): ONE unit-stride problem
@@ -464,9 +461,7 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   IgemmArgs& a = P.a;
   // unit-stride grids, and stride 2 in both directions (halo (2·th + k − 2) x (2·tw + k − 2))
   const int S = a.ist_h;
-  static const bool no_s2 = getenv("TPG_HALO_NO_S2") != nullptr;  // (A/B hook)
-  static const int min_c = getenv("TPG_HALO_MINC") ? atoi(getenv("TPG_HALO_MINC")) : 1;  // (A/B hook)
-  if (a.ntaps < 1 || a.C < min_c || a.ist_h != a.ist_w || (S != 1 && (S != 2 || no_s2))) return;
+  if (a.ntaps < 1 || a.C < 1 || a.ist_h != a.ist_w || (S != 1 && S != 2)) return;
   int dymin = 127, dymax = -128, dxmin = 127, dxmax = -128;
   for (int t = 0; t < a.ntaps; ++t) {
     dymin = std::min<int>(dymin, a.dy[t]); dymax = std::max<int>(dymax, a.dy[t]);
@@ -481,26 +476,23 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   int bn;
   if (a.Nout <= 32) bn = 32;
   else if (a.Nout <= 64) bn = 64;
-  else if (a.Nout <= 80 && !getenv("TPG_HALO_NO80")) bn = 80;  // (A/B hook)
+  else if (a.Nout <= 80) bn = 80;
   else if (a.Nout <= 96) bn = 96;
   else if (a.Nout <= 128) bn = 128;
   else if (a.Nout > 192 && a.Nout <= 208) bn = 208;
   else {
     // fewest padded columns among the 128 / 192 / 224 tiles, the wider tile on ties
     // (measured: enhance_16 768->768 at 16x16 -24 %, the 8x8 576-channel layers +6 µs)
-    static const bool no192 = getenv("TPG_HALO_NO192") != nullptr;  // (A/B hook)
     int64_t best = -1;
     for (int c : {224, 192, 128}) {
-      if (c == 192 && no192) continue;
       const int64_t pad = rup(a.Nout, c);
       if (best < 0 || pad < best) { best = pad; bn = c; }
     }
   }
-  static const bool no512 = getenv("TPG_HALO_NO512") != nullptr;  // (A/B hook)
   // (not for deep inputs: conv5_0's 206 -> 64 forward measured 0.43 -> 0.46 ms with it, against
   // add_128 0.59 -> 0.49 and conv0_res 0.35 -> 0.27)
   if (S == 2 && bn > 128) bn = 128;  // (the 1024-pixel halo leaves LDS for 128-row weight slices)
-  const int bm = (!no512 && S == 1 && halo_cfg512(bn) >= 0 && dtype != TPG_F32 && (int64_t)N * JH * JW >= 512 * 512 &&
+  const int bm = (S == 1 && halo_cfg512(bn) >= 0 && dtype != TPG_F32 && (int64_t)N * JH * JW >= 512 * 512 &&
                   JW >= 64 && cdiv(a.Nout, bn) == 1 && a.C <= 128) ? 512 : 256;
   const int HCAP = (bm == 512 || S == 2) ? 1024 : 5 * 128;
   int bth = 0, btw = 0, bimg = 0;
@@ -544,8 +536,6 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   h.TH = bth; h.TW = btw; h.IMG = bimg; h.SH = S; h.SW = S; h.dil = a.dil;
   h.HH = (bth - 1) * S + sy; h.HW = (btw - 1) * S + sx;
   h.hcap = hcap;
-  static const int halo_var = getenv("TPG_HALO_VAR") ? atoi(getenv("TPG_HALO_VAR")) : 0;  // tuning
-  h.var = halo_var;
   for (int t = 0; t < a.ntaps; ++t) h.toff[t] = (a.dy[t] - dymin) * h.HW + (a.dx[t] - dxmin);
   h.pad_mode = a.pad_mode;
   h.N = N; h.JH = JH; h.JW = JW;
@@ -555,9 +545,7 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   // split over k-steps until the grid covers the chip (each split >= 4 pipeline steps)
   const int64_t base = (((int64_t)N * h.tiles_h * h.tiles_w + bimg - 1) / bimg) * h.ntiles;
   int ks = 1;
-  static const int split_below = getenv("TPG_SPLIT_BELOW") ? atoi(getenv("TPG_SPLIT_BELOW")) : 256;  // tuning
-  static const int split_to = getenv("TPG_SPLIT_TO") ? atoi(getenv("TPG_SPLIT_TO")) : 256;
-  static const int split_steps = getenv("TPG_SPLIT_STEPS") ? atoi(getenv("TPG_SPLIT_STEPS")) : 4;
+  constexpr int split_below = 256, split_to = 256, split_steps = 4;  // (swept in round 2: best)
   // (deterministic mode: no k-split at all, so a sample's outputs are summed in the same
   // order whatever the batch size — the DP run then matches the 1-GPU run at its global batch)
   if (base < split_below / g_share && !deterministic()) {
@@ -757,7 +745,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
   const bool vA = vec_ok(A, dtype);
   if (mk) {  // the mask mode has no generic-kernel fallback: decide before launching anything
     // (the 512-row and stride-2 halo configs, ids >= 24, have no masked variant)
-    if (v.size() != 1 || !v[0].halo || v[0].hcfg >= 24 || v[0].h.ntaps < 2 || (v[0].h.var & 2) || !vA) return -31;
+    if (v.size() != 1 || !v[0].halo || v[0].hcfg >= 24 || v[0].h.ntaps < 2 || !vA) return -31;
     const int64_t ext = (int64_t)(v[0].h.N - 1) * std::abs(A.stride[0]) + (int64_t)(v[0].h.A_H - 1) * std::abs(A.stride[2]) +
                         (int64_t)(v[0].h.A_W - 1) * std::abs(A.stride[3]) + v[0].h.C + 64;
     const int64_t extm = (int64_t)(v[0].h.N - 1) * mk->M.stride[0] + (int64_t)(v[0].h.A_H - 1) * mk->M.stride[2] +
@@ -1147,9 +1135,8 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
   a.div_phpw.init(a.PH * a.PW);
   // kernel-row halo kernel (stride-1 Conv2d, bf16, 64-pixel row segments): algo 6, and the
   // default for untuned calls when it applies
-  static const bool rh_on = !getenv("TPG_WGRAD_RH") || atoi(getenv("TPG_WGRAD_RH")) != 0;  // A/B hook
   const bool rh_algo = d->algo >= 6 && d->algo <= 12;
-  if (((d->algo == 0 && rh_on) || rh_algo) && !comp && !d->transposed) {
+  if ((d->algo == 0 || rh_algo) && !comp && !d->transposed) {
     const int rc = wgrad_rh(d, x, g, dw, dbias, (hipStream_t)stream);
     if (rc != 1) {
       *bias_done = rc == 0 && dbias != nullptr;
@@ -1185,12 +1172,6 @@ static int32_t bwd_filter_impl(const tpg_conv_desc* d, const tpg_tensor& x, cons
     if (d->algo >= 1 && d->algo <= 5 && d->ksplit >= 1) {
       bm = cand[d->algo - 1][0]; bn = cand[d->algo - 1][1];
       bks = std::min(d->ksplit, nkt);
-    }
-    if (const char* f = getenv("TPG_WGRAD_FORCE")) {  // tuning hook: "bm,bn,ks"
-      int fm = 0, fn = 0, fk = 0;
-      if (sscanf(f, "%d,%d,%d", &fm, &fn, &fk) == 3 && wgrad2_cfg(fm, fn) >= 0 && fk >= 1) {
-        bm = fm; bn = fn; bks = std::min(fk, nkt);
-      }
     }
     if (deterministic()) bks = 1;
     a.pix_per_split = (int)rup(cdiv(a.npix, bks), kp);
@@ -1272,13 +1253,10 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   // (round 1 measured 42.1 ms/step with maps up to 64 x 64, 42.5 with every map, 43.0 with
   // none; after the 512-row and stride-2 tiles -- which have no masked variant and now fall
   // back to the separate pass -- every map measured 37.39 vs 37.54 / 37.56 at 64 x 64)
-  static const int64_t mask_maxpix = getenv("TPG_MASK_MAXPIX") ? atoll(getenv("TPG_MASK_MAXPIX")) : 1 << 30;
   if (!have_g && dx.data && !d->transposed && d->stride_h == 1 && d->stride_w == 1 && d->pad_mode == TPG_PAD_ZERO &&
-      (int64_t)d->out_h * d->out_w <= mask_maxpix &&
       d->in_h == d->out_h && d->in_w == d->out_w && gy.dtype == d->dtype && y.dtype == d->dtype &&
       dx.dtype == d->dtype && vec_ok(gy, d->dtype) && vec_ok(y, d->dtype) && vec_ok(g, d->dtype) &&
-      y.stride[0] == g.stride[0] && y.stride[2] == g.stride[2] && y.stride[3] == g.stride[3] &&
-      !getenv("TPG_NO_MASKED_DGRAD")) {
+      y.stride[0] == g.stride[0] && y.stride[2] == g.stride[2] && y.stride[3] == g.stride[3]) {
     const bool packed = d->flags & TPG_FLAG_WPACKED;
     if (w.data && (w.dtype == TPG_F32 || packed) && !bwd_data_composite(d, &gy, &dx)) {
       std::vector<Prob> v = plan_bwd_data(d, false);

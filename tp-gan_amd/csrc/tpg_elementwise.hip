@@ -594,15 +594,9 @@ static bool pix_dense_any(const tpg_tensor& t, int h, int w) {
   return t.stride[1] == 1 && t.stride[2] == t.stride[3] * w && t.stride[0] == t.stride[2] * h;
 }
 
-// act_bwd grid shaping (env knobs for tuning): pixels per lane, block cap
-static int act_ppl() {
-  static const int v = getenv("TPG_ACTB_PPL") ? atoi(getenv("TPG_ACTB_PPL")) : 4;
-  return v < 1 ? 1 : v;
-}
-static int act_cap() {
-  static const int v = getenv("TPG_ACTB_CAP") ? atoi(getenv("TPG_ACTB_CAP")) : 1024;
-  return v < 1 ? 1 : v;
-}
+// act_bwd grid shaping: pixels per lane, block cap
+static int act_ppl() { return 4; }
+static int act_cap() { return 1024; }
 
 
 static bool pix_dense_vec(const tpg_tensor& t, int h, int w, int dtype, int c) {
@@ -681,11 +675,10 @@ int launch_act_vec_group(const ActVecArgs* a, int n, int dtype, hipStream_t s) {
 extern "C" int32_t tpg_act_bwd_impl(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope,
                                      tpg_tensor gy, tpg_tensor y, tpg_tensor g, float* dbias, hipStream_t s) {
   const int dt = g.dtype;
-  static const bool force_scalar = getenv("TPG_ACTB_SCALAR") != nullptr;  // debug switch
   ActVecArgs a;
-  if (!force_scalar && act_vec_args(n, c, h, w, act, slope, gy, y, g, dbias, &a) == 0) return launch_act_vec(a, dt, s);
+  if (act_vec_args(n, c, h, w, act, slope, gy, y, g, dbias, &a) == 0) return launch_act_vec(a, dt, s);
   int64_t npix = (int64_t)n * h * w;
-  if (!force_scalar && c <= 256 && pix_dense_any(gy, h, w) && pix_dense_any(g, h, w) &&
+  if (c <= 256 && pix_dense_any(gy, h, w) && pix_dense_any(g, h, w) &&
       (act == TPG_ACT_NONE || pix_dense_any(y, h, w))) {
     const int ppi = 256 / c;
     const int64_t blocks = (dbias && deterministic()) ? 1 :

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const int hcap = p.hcap;
-  const int RS = (p.var & 2) ? 4 : 3;                  // weight ring slots (one tap slice each)
+  constexpr int RS = 3;                                // weight ring slots (one tap slice each)
   u32x4* halo = lds;                                   // [2][hcap][4]
   u32x4* wts = lds + 2 * hcap * 4;                     // [RS][BNL][4] ring
   int* s_toff = reinterpret_cast<int*>(wts + RS * BNL * 4);  // [TPG_MAX_TAPS]
@@ -282,8 +282,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Stagger (bf16, BN >= 128 tiles, which run one block per CU anyway; var bit 8 turns it
-  // off): waves 4-7 carry the MFMAs of B fragments NH.. of every step over the barrier
+  // Stagger (bf16, BN >= 128 tiles, which run one block per CU anyway): waves 4-7 carry the MFMAs of B fragments NH.. of every step over the barrier
   // (operands held in registers, +28 VGPRs) and issue them first in the next step, so each
   // SIMD has matrix work while its partner wave waits for the step's fragment reads
   // (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Measured ~1 % on the 128x128 layers.
@@ -296,7 +295,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   constexpr bool LAG_OK = false;
 #endif
   constexpr int NH = LAG_OK ? (NREP + 1) / 2 : NREP;
-  const bool lag = LAG_OK && !(p.var & 8) && wave >= 4;
+  const bool lag = LAG_OK && wave >= 4;
   u32x4 ha[MREP], hb[NREP - NH + 1];
 #pragma unroll
   for (int m = 0; m < MREP; ++m) ha[m] = u32x4{0u, 0u, 0u, 0u};
@@ -378,32 +377,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   const int ntaps = p.ntaps;
   const int total = nks * ntaps;
   __syncthreads();  // tap table
-  if ((p.var & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  if (total > 0 && RS == 4 && !MASK) {
-    // 4-slot ring: step s+3's weights are issued at the start of step s
-    load_halo(0);
-    issue_w(0, 0);
-    issue_w(min(1, total - 1), 1);
-    issue_w(min(2, total - 1), 2);
-    store_halo(0);
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    int ks = 0, t = 0, slot = 0;
-    int toff = s_toff[0];
-    for (int s = 0; s < total; ++s) {
-      const bool more_ks = ks + 1 < nks;
-      if (t == 0 && more_ks) load_halo(ks + 1);
-      issue_w(min(s + 3, total - 1), (slot + 3) & 3);
-      const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];
-      compute(ks & 1, slot, toff);
-      toff = toff_next;
-      if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
-      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
-      slot = (slot + 1) & 3;
-      if (++t == ntaps) { t = 0; ++ks; }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if (total > 0) {
+  if (total > 0) {
     load_halo(0);
     issue_m(0, 0);
     issue_w(0, 0);
@@ -626,8 +600,9 @@ int halo_cfg(int hl, int bn) {
 }
 
 // Pipeline variants measured and dropped: two taps per barrier with a 6-slot ring (+5 % on
-// 7x7 layers alone, -2 % on the train step) and a cross-barrier fragment prefetch with a
-// 4-slot ring (-2..12 %: the second fragment set pushed the 224-wide tile past 256 VGPRs).
+// 7x7 layers alone, -2 % on the train step), a cross-barrier fragment prefetch with a
+// 4-slot ring (-2..12 %: the second fragment set pushed the 224-wide tile past 256 VGPRs),
+// waves 4-7 at a raised priority (no gain; removed in round 4 with the other variant bits).
 size_t halo_lds_bytes(int hcap, int bn, int rs, int bm) {
   return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn, bm));
 }
@@ -635,7 +610,7 @@ size_t halo_lds_bytes(int hcap, int bn, int rs, int bm) {
 template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
 static int launch_halo_t(const Grouped<HaloArgs, NG>& g, dim3 grid, size_t lds, hipStream_t s) {
   auto k = halo_kernel<DT, HL, BN, WM, WN, MASK, BM, NG>;
-  const int maxl = (int)halo_lds_bytes(HL * 128, BN, HL == 8 ? 3 : 4, BM);  // (1024-pixel halos: 3-slot ring only)
+  const int maxl = (int)halo_lds_bytes(HL * 128, BN, 3, BM);
   static bool once = ((void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, maxl),
                       true);
   (void)once;
@@ -648,7 +623,7 @@ static int launch_halo_t(const HaloArgs& a, dim3 grid, hipStream_t s) {
   Grouped<HaloArgs, 1> g;
   g.a[0] = a;
   g.boff[0] = 0; g.boff[1] = (int)(grid.x * grid.y * grid.z); g.nm = 1;
-  return launch_halo_t<DT, HL, BN, WM, WN, MASK, BM, 1>(g, grid, halo_lds_bytes(a.hcap, a.BN, (a.var & 2) ? 4 : 3, BM),
+  return launch_halo_t<DT, HL, BN, WM, WN, MASK, BM, 1>(g, grid, halo_lds_bytes(a.hcap, a.BN, 3, BM),
                                                         s);
 }
 
@@ -663,7 +638,7 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
   dim3 grid((a.N * a.tiles_h * a.tiles_w + a.IMG - 1) / a.IMG, a.ntiles, a.ksplit);
   // mask mode: one k-step's y chunks must land (LDS-DMA issued at tap 0) before its halo is
   // staged (last tap): at least two taps, the 3-slot ring, whole 16-pixel DMA rows
-  if (mask && (a.ntaps < 2 || (a.var & 2) || a.hcap % 16 || a.SH != 1 || a.SW != 1)) return -1;
+  if (mask && (a.ntaps < 2 || a.hcap % 16 || a.SH != 1 || a.SW != 1)) return -1;
 #define X(id, HL_, BN_, WM_, WN_)                                                          \
   if (cfg == (id)) {                                                                       \
     if (a.hcap > HL_ * 128) return -1;                                                     \
@@ -678,7 +653,7 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
 #undef X
 #define X(id, HL_, BN_, WM_, WN_)                                                          \
   if (cfg == (id)) {                                                                       \
-    if (a.hcap > HL_ * 128 || mask || (a.var & 2)) return -1;                              \
+    if (a.hcap > HL_ * 128 || mask) return -1;                              \
     return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, false, 512>(a, grid, s)       \
          : dtype == 2 ? launch_halo_t<2, HL_, BN_, WM_, WN_, false, 512>(a, grid, s)       \
                       : launch_halo_t<0, HL_, BN_, WM_, WN_, false, 512>(a, grid, s);      \
@@ -687,7 +662,7 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask)
 #undef X
 #define X(id, HL_, BN_, WM_, WN_)                                                          \
   if (cfg == (id)) {                                                                       \
-    if (a.hcap > HL_ * 128 || mask || (a.var & 2)) return -1;                              \
+    if (a.hcap > HL_ * 128 || mask) return -1;                              \
     return dtype == 1 ? launch_halo_t<1, HL_, BN_, WM_, WN_, false>(a, grid, s)            \
          : dtype == 2 ? launch_halo_t<2, HL_, BN_, WM_, WN_, false>(a, grid, s)            \
                       : launch_halo_t<0, HL_, BN_, WM_, WN_, false>(a, grid, s);           \
@@ -727,7 +702,7 @@ int launch_halo_group(const HaloArgs* a, int n, int dtype, int cfg, hipStream_t 
   int hcap = 0, blocks = 0;
   for (int m = 0; m < n; ++m) {
     const HaloArgs& h = a[m];
-    if (h.BN != a[0].BN || (h.var & 2) || h.var != a[0].var) return -1;
+    if (h.BN != a[0].BN) return -1;
     if (mask && (h.ntaps < 2 || h.hcap % 16 || h.SH != 1 || h.SW != 1)) return -1;
     g.a[m] = h;
     g.boff[m] = blocks;

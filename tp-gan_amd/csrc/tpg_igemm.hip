@@ -277,10 +277,17 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
   const int JHJW = p.JH * p.JW;
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
+  const bool small = (int64_t)p.M * p.Nout < (1ll << 31);  // 32-bit index math (uniform)
   for (int64_t idx = b0 * blockDim.x + threadIdx.x; idx < total; idx += nb * blockDim.x) {
     const int64_t e0 = idx * V;
-    int row = (int)(e0 / p.Nout);
-    int col = (int)(e0 - (int64_t)row * p.Nout);
+    int row, col;
+    if (small) {
+      row = (int)e0 / p.Nout;
+      col = (int)e0 - row * p.Nout;
+    } else {
+      row = (int)(e0 / p.Nout);
+      col = (int)(e0 - (int64_t)row * p.Nout);
+    }
     int n = row / JHJW;
     int rem = row - n * JHJW;
     int j = rem / p.JW, i = rem - j * p.JW;
@@ -299,6 +306,38 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
     }
     const int64_t yo = (int64_t)n * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw + col;
     const int64_t ro = (int64_t)n * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw + col;
+    if constexpr (V == 4 && sizeof(E) == 2) {
+      // four 16-bit outputs as one 8-byte store (and an 8-byte residual load) when aligned
+      // (the four halves are taken apart as scalars: this hipcc compiles
+      // __builtin_bit_cast(E, vec[u]) of an ext_vector element as element 0 for every u --
+      // the parked round-3 version of this path read the first residual four times)
+      if (((yo | (R ? ro : 0)) & 3) == 0) {
+        uint2 rw = make_uint2(0u, 0u);
+        if (R) rw = *reinterpret_cast<const uint2*>(R + ro);
+        uint32_t ow[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t w = h ? rw.y : rw.x;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int u = 2 * h + e;
+            float x = v[u];
+            if (p.bias) x += p.bias[p.bias_mod ? (col + u) % p.bias_mod : col + u];
+            if (R) {
+              const unsigned short r16 = (unsigned short)(e ? (w >> 16) : (w & 0xffffu));
+              x += p.res_scale * (float)__builtin_bit_cast(E, r16);
+            }
+            const E o = (E)act_apply(x, p.act, p.slope);
+            const unsigned short o16 = __builtin_bit_cast(unsigned short, o);
+            packed |= (uint32_t)o16 << (16 * e);
+          }
+          ow[h] = packed;
+        }
+        *reinterpret_cast<uint2*>(Y + yo) = make_uint2(ow[0], ow[1]);
+        continue;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       float x = v[u];

@@ -380,9 +380,6 @@ struct HaloArgs {
   int act;
   float slope;
   int yvec, rvec, wvec;       // 16-byte output / residual / partial-slice stores allowed
-  int var;                    // pipeline variant bits (TPG_HALO_VAR, tuning): 1 = waves 4-7 at
-                              // priority 1, 2 = 4-slot weight ring (DMA three steps ahead),
-                              // 8 = no wave stagger (bf16 BN >= 128 tiles stagger waves 4-7)
   // Masked input-gradient mode (launch_halo(..., mask = true); stride-1 "same" Conv2d dgrad):
   // A holds the incoming gradient gy, M the conv's saved output y (same grid); the halo is
   // staged as g = gy * act'(y) (mact / mslope), and every g chunk of the block's own output

@@ -97,11 +97,11 @@ def deterministic(on=True):
 
 
 # Run the Generator's four local pathways on side streams (D_and_G_model.Generator).
-MULTISTREAM = os.environ.get("TPG_MULTISTREAM", "1") != "0"
+MULTISTREAM = True
 # Ops created inside `concurrent()` carry TPG_FLAG_CONCURRENT: their grids are planned for a
 # share of the chip (the side-stream local pathways), forward and backward.
 _CONCURRENT = [False]
-CONCURRENT_HINT = {"enabled": os.environ.get("TPG_CONCURRENT_HINT", "1") != "0"}
+CONCURRENT_HINT = {"enabled": True}
 
 
 @contextlib.contextmanager
@@ -119,8 +119,8 @@ _SIDE = {}
 # overlaps this layer's weight gradient; leaving the block joins the side stream.
 # (off by default: measured 37.86 / 37.97 ms/step with it vs 37.80 without -- the overlap
 # it buys is paid back in host time per layer (event, wait, record_stream), and the host
-# already spends ~31.6 ms enqueueing a ~38 ms step; TPG_WGRAD_SIDE=1 turns it on)
-WGRAD_SIDE = {"stream": None, "enabled": os.environ.get("TPG_WGRAD_SIDE", "0") != "0"}
+# already spends ~31.6 ms enqueueing a ~38 ms step; WGRAD_SIDE["enabled"] = True turns it on)
+WGRAD_SIDE = {"stream": None, "enabled": False}
 
 
 @contextlib.contextmanager
@@ -148,11 +148,9 @@ def side_streams(device, n, tag=""):
     return _SIDE[key]
 
 
-# HIP stream priorities of the side streams (lower = higher priority).  The local pathways'
-# backward runs beside the global pathway's and, sharing the CUs with it, used to finish ~1 ms
-# after it (the G Adam waited for it: profiles/r03 stream split); at high priority their
-# workgroups are dispatched first and the global chain fills the rest of the chip.
-SIDE_PRIORITY = {"local": int(os.environ.get("TPG_LOCAL_PRIORITY", "0"))}
+# HIP stream priorities of the side streams (lower = higher priority).  (High priority for the
+# local pathways measured 36.13 vs 35.90-35.95 ms/step in round 3: default priority.)
+SIDE_PRIORITY = {"local": 0}
 
 
 _ROCTX = [None]
@@ -277,9 +275,9 @@ class ConvGeom:
 # scratch gradient (HIP events, device synchronised around each trial, so only during
 # warm-up).  bf16 only; the cache can be saved / loaded as JSON for reproducible runs.
 AUTOTUNE = {"enabled": True, "cache": {}, "trials": 0}
-# (A/B hook TPG_WG_SPLITS; adding 0 = the library's own split for each tile, which fills whole
-# rounds of the chip and won several isolated trials, measured 36.22-36.26 vs 36.10-36.14 ms/step)
-_WG_SPLITS = tuple(int(v) for v in os.environ.get("TPG_WG_SPLITS", "1,2,4,8,16,32,64").split(","))
+# (adding the library's own split for each tile, which fills whole rounds of the chip and won
+# several isolated trials, measured 36.22-36.26 vs 36.10-36.14 ms/step in round 3)
+_WG_SPLITS = (1, 2, 4, 8, 16, 32, 64)
 
 
 def _desc_tuple(d):
@@ -314,7 +312,7 @@ def _wgrad_key(d):
     return ("wgrad", _desc_tuple(d) + (int(d.flags & FLAG_CONCURRENT),))
 
 
-_TUNE_GRAPH = os.environ.get("TPG_TUNE_GRAPH", "1") != "0"
+_TUNE_GRAPH = True
 _TUNE_REPS = 4
 _TUNE_STREAMS = {}
 
@@ -332,7 +330,7 @@ def _time_wgrad(lib, d, x, g, scratch):
     captured into one HIP graph, replayed twice, the second replay timed -- the GPU's time
     alone.  (Eager event pairs around one launch also time the host's ~20 us ctypes issue of
     the launch, comparable to a small layer's whole weight gradient, so candidates a few us
-    apart were ranked by host jitter; TPG_TUNE_GRAPH=0 restores that timing for A/B.)"""
+    apart were ranked by host jitter; _TUNE_GRAPH = False restores that timing for A/B.)"""
     if not _TUNE_GRAPH:
         ms = []
         for rep in range(2):
@@ -725,31 +723,48 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
     split = (side is not None and not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
              ctx.link_res is None and not ctx.geom.transposed and PROBE["match"] is None and
              not torch.cuda.is_current_stream_capturing())
+    # probing the weight gradient (bench.py roofline, tools/trace_step.py): the same two calls
+    # as the side-stream split, both on this stream, events around the second -- the kernels
+    # and their order on the stream are the fused call's (input gradient, then weight gradient)
+    probe_w = (not split and not grouped and dwt is not None and (dbias is None or fused_b) and
+               not ctx.geom.transposed and PROBE["match"] is not None and PROBE["match"](d, "wgrad") and
+               not torch.cuda.is_current_stream_capturing())
+    if probe_w:
+        split = True
     e0 = _probe_begin(d, "bwd")
     _run_maybe_packed(
         lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk), tt(y), tt(gy), tt(g), tt(fx),
                                    tt(None if split else dwt), None if split else bptr, wsp, wsn, stream_ptr()),
         lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), tt(wv), tt(y), tt(gy), tt(g), tt(fx),
                                    tt(None if split else dwt), None if split else bptr, wsp, wsn, stream_ptr()), d, pk)
-    _probe_end(e0, d, "bwd", _conv_flops(d) * (int(bool(need_dx)) + int(bool(need_dw and not tune_first))))
+    _probe_end(e0, d, "bwd", _conv_flops(d) * (int(bool(need_dx)) + int(bool(need_dw and not tune_first and not split))))
     d.flags = d.flags & ~FLAG_DX_ACCUM
     if grouped:
         keep += [ws, g, gy, wv]
     if split:
         gt = gy if g_is_gy else g  # (g now holds act'(y) * gy: the second call takes it as is)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
-        side.wait_event(ev)
         d2 = _plain_desc(d)
         d2.algo, d2.ksplit = d.algo, d.ksplit
-        with torch.cuda.stream(side):
+        if probe_w:
+            ew = _probe_begin(d, "wgrad")
             check(lib.tpg_conv2d_bwd(ctypes.byref(d2), tt(x), tt(None), tt(None), tt(gt), tt(gt), tt(None), tt(dwt),
                                      bptr, None, 0, stream_ptr()))
+            _probe_end(ew, d, "wgrad")
             if fused_b:
                 _grad_ready(ctx.bparam)
             _grad_ready(ctx.wparam)
-        for t in (x, gt):  # (their memory stays reserved until the side stream has read it)
-            t.record_stream(side)
+        else:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                check(lib.tpg_conv2d_bwd(ctypes.byref(d2), tt(x), tt(None), tt(None), tt(gt), tt(gt), tt(None),
+                                         tt(dwt), bptr, None, 0, stream_ptr()))
+                if fused_b:
+                    _grad_ready(ctx.bparam)
+                _grad_ready(ctx.wparam)
+            for t in (x, gt):  # (their memory stays reserved until the side stream has read it)
+                t.record_stream(side)
         fused_b = False
         dbias = None  # (accumulated into the flat buffer on the side stream)
         dw = None
@@ -975,7 +990,7 @@ def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_Z
 # LocalPathways, D_and_G_model.py:18-110), whose forward and backward each run inside one
 # tpg_group_begin / tpg_group_end scope: every kernel position becomes ONE grid over all members
 # instead of one small launch per patch.  GROUP["enabled"] = False: per-member _ConvAct nodes.
-GROUP = {"enabled": os.environ.get("TPG_NO_GROUP") is None}
+GROUP = {"enabled": True}
 
 
 class _MemberCtx(object):
@@ -1063,7 +1078,7 @@ def conv2d_group(calls):
     return list(_ConvActGroup.apply(specs, *flat))
 
 
-RES_LINK = {"enabled": not os.environ.get("TPG_NO_RES_LINK")}  # (A/B, tests: off = autograd sums it)
+RES_LINK = {"enabled": True}  # (A/B, tests: off = autograd sums it)
 
 
 class _FoldTaps(torch.autograd.Function):
@@ -1103,7 +1118,7 @@ class _UnfoldTaps(torch.autograd.Function):
         return _FoldTaps.apply(g, fh, fw, sh, sw, pt, pl, oh, ow), None, None
 
 
-FOLD = {"enabled": os.environ.get("TPG_NO_FOLD") is None}
+FOLD = {"enabled": True}
 
 
 def folded_args(x, weight, stride, pad):
@@ -1183,7 +1198,7 @@ class _FlattenNCHW(torch.autograd.Function):
 # of an HxW full-kernel conv on the channels-last map, so its weight gradient walks the weight
 # in its own (NCHW) order -- coalesced rows instead of 4-byte accesses 256 B apart (the
 # full-kernel form's weight-gradient launch took 0.34 ms for 67 MB)
-LINEAR_FLAT = {"enabled": os.environ.get("TPG_LINEAR_FULLKERNEL", "0") == "0"}
+LINEAR_FLAT = {"enabled": True}
 
 
 def linear(x, weight, bias=None, act=None, image_hw=None):
@@ -1443,7 +1458,7 @@ def bn_fold(weight, bias, bn):
     return wf, bf
 
 
-_FOLD_CACHE = os.environ.get("TPG_FOLD_CACHE", "1") != "0"  # (A/B hook)
+_FOLD_CACHE = True
 
 
 class _FrozenPack:

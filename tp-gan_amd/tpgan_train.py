@@ -42,7 +42,8 @@ class FlatParams:
         self.exp_avg = torch.zeros_like(self.data)
         self.exp_avg_sq = torch.zeros_like(self.data)
         self.adam_state = torch.zeros(4, dtype=torch.float32, device=device)  # {step, bias corrections}
-        self.step = 0
+        self.step = 0             # host count of adam() calls; adam_state[0] (device) is the optimizer's
+        self.skipped = torch.zeros((), dtype=torch.float32, device=device)  # fp16 steps skipped as non-finite
         self.epoch = 0            # bumped by every optimizer update (pre-packed weight images follow it)
         self.layout_version = 0   # bumped by relayout(): captured hipGraphs hold the old buffers
         self.pack_entries = {}    # tpgan_ops pre-packed weight images of this network's convs
@@ -107,8 +108,17 @@ class FlatParams:
             tpgan_ops.grad_check(self.grad, self.adam_state)
         tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
                             weight_decay, self.adam_state, 0, grad_scale)
+        if check_finite:  # (on the device: no synchronisation; skipped_steps() reads it)
+            self.skipped.add_(self.adam_state[3].ne(0).float())
         self.epoch += 1
         tpgan_ops.repack(self)
+
+    def skipped_steps(self):
+        """Updates skipped for non-finite gradients so far (synchronises).  A run whose static
+        loss scale keeps overflowing stops learning; this is the signal.  The step counter that
+        drives Adam's bias correction is adam_state[0], which a skipped update leaves alone
+        (self.step counts adam() calls, skipped or not)."""
+        return int(self.skipped.item())
 
     def last_step_skipped(self):
         """True when the last adam(check_finite=True) found non-finite gradients (synchronises)."""
@@ -287,7 +297,7 @@ class OverlappedGradSync(GradSync):
         if not self.active:
             return
         i = self.index.get(id(p))
-        if i is None or i in self.seen:
+        if i is None or (i in self.seen and not self.count_accumulate):
             return
         b = self.bucket_of[i]
         if self.flat.grad.is_cuda:  # (one event per contribution: they may come from several streams)
@@ -301,6 +311,11 @@ class OverlappedGradSync(GradSync):
                 return
             if self.counts[i] < self.expected[i]:
                 return
+            if self.counts[i] > self.expected[i]:
+                # a contribution beyond what the learning step observed: the parameter's bucket
+                # may already be in flight, so this add would race its all-reduce
+                raise RuntimeError("OverlappedGradSync: parameter %d got %d gradient contributions, the first "
+                                   "step observed %d" % (i, self.counts[i], self.expected[i]))
         self.seen.add(i)
         self.order.append(i)
         self.pending[b] -= 1
@@ -332,6 +347,12 @@ class OverlappedGradSync(GradSync):
             self.expected = list(self.counts)
             self.order = sorted((i for i in range(len(self.counts)) if self.counts[i] > 0),
                                 key=lambda i: self.last_seq[i])
+        elif self.count_accumulate:
+            bad = [i for i in range(len(self.counts)) if self.counts[i] != self.expected[i]]
+            if bad:
+                raise RuntimeError("OverlappedGradSync: gradient contribution counts changed since the first step "
+                                   "(parameters %s: %s, expected %s)" % (bad[:5], [self.counts[i] for i in bad[:5]],
+                                                                          [self.expected[i] for i in bad[:5]]))
         cur = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
         while self.next < len(self.buckets):
             self._issue(self.next, after_stream=cur)
@@ -416,6 +437,7 @@ class TPGANTrainer:
         # in data-parallel runs, where that tail is the all-reduce's
         self.real_ahead = (self.world > 1) if real_ahead is None else bool(real_ahead)
         self._d_real_next = None
+        self.real_ahead_used = 0  # steps whose D(real) came from the previous step's real_ahead pass
         self._capturing = False
         self._segmented = False
         self.identity_fn = identity_fn
@@ -443,10 +465,15 @@ class TPGANTrainer:
         # D(real) of this batch already ran at the end of the previous step (_real_ahead): its
         # gradient is in fD.grad and its output is kept for the loss
         d_real_pre, self._d_real_next = self._d_real_next, None
-        if d_real_pre is not None and d_real_pre[0] is not b["frontal"]:
-            d_real_pre = None  # (the caller's next batch was not the one it announced)
+        if d_real_pre is not None and (d_real_pre[0] is not b["frontal"] or
+                                       d_real_pre[1] != self._real_key(b["frontal"])):
+            # (the caller's next batch was not the one it announced, its images were refilled in
+            # place since, or D's weights changed after the pass: a checkpoint load, a relayout)
+            d_real_pre = None
         if d_real_pre is None:
             self.fD.zero_grad()
+        else:
+            self.real_ahead_used += 1
         # the identity loss's real-image features run on a side stream under G's forward
         # (not while phase A is captured as a graph of its own: the fork would stay unjoined
         # at the end of that capture, and phase B's graph would wait on work of another graph)
@@ -466,7 +493,7 @@ class TPGANTrainer:
                     d_both = D(torch.cat([real, fake.detach()], 0)).float()
                     d_real, d_fake = d_both[:B], d_both[B:]
                 else:
-                    d_real, d_fake = d_real_pre[1], D(fake.detach()).float()
+                    d_real, d_fake = d_real_pre[2], D(fake.detach()).float()
                 loss_D = d_fake.mean() - d_real.mean()
                 if self.gp:
                     loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
@@ -489,7 +516,14 @@ class TPGANTrainer:
             loss = -d_real.mean()
             with tpgan_ops.wgrad_side_stream():
                 (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
-        self._d_real_next = (nb["frontal"], d_real.detach())
+        self._d_real_next = (nb["frontal"], self._real_key(nb["frontal"]), d_real.detach())
+
+    def _real_key(self, frontal):
+        """What a precomputed D(real) pass is valid for: the very tensor (identity, storage
+        address, in-place version counter -- a caller refilling one persistent batch buffer
+        bumps it) and D's weights (FlatParams.epoch / layout_version: every optimizer update,
+        load or relayout changes them)."""
+        return (frontal.data_ptr(), frontal._version, self.fD.epoch, self.fD.layout_version)
 
     def gradient_penalty(self, real, fake, alpha=None):
         """WGAN-GP (config.py:72 weight_gradient_penalty): mean over the batch of
@@ -554,7 +588,10 @@ class TPGANTrainer:
         with tpgan_ops.roctx_range("G-adam"):
             self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
                          check_finite=self.loss_scale != 1.0)
-        return {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
+        out = {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
+        if self.loss_scale != 1.0:  # device tensors: reading them is the caller's synchronisation
+            out["skipped_D"], out["skipped_G"] = self.fD.skipped, self.fG.skipped
+        return out
 
     # ---- checkpoint / resume.  Files and formats of the reference's
     # UtilityMethods.save_model / save_optimizer (UtilityMethods.py:58-103), one directory per
@@ -628,6 +665,7 @@ class TPGANTrainer:
                     raise ValueError("checkpoint %s/%s: %s has shape %s, model %s" %
                                      (tag, epoch, k, tuple(v.shape), tuple(own[k].shape)))
             loaded.append((net, flat, ck))
+        self._d_real_next = None  # (a D(real) pass precomputed with the old weights)
         if adopt:
             self.lr = float(adopt.get("lr", self.lr))
             self.betas = tuple(adopt.get("betas", self.betas))
@@ -659,6 +697,7 @@ class TPGANTrainer:
         weight-gradient autotuner, and train the model) run on a side stream first, as
         capture requires."""
         self._static = {k: v.clone() for k, v in b.items()}
+        self._d_real_next = None  # (graph replays never run the eager real_ahead pass)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         # the data-parallel bucket layout is re-learned after the first overlapped step
