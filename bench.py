@@ -10,10 +10,11 @@ with fp32 accumulate and fp32 master weights, synthetic Multi-PIE-shaped data re
 HBM, random-init weights.  Data parallel over N GPUs (one process per GPU, RCCL
 all-reduce of G and D gradients): per-GPU batch fixed, so scaling is weak.
 
-Rank 0 prints one JSON line.  `roofline` is for the dominant kernel (the 5x5 206->206
-enhance_features_128 convolution forward, timed with HIP events around its launches on
-the launching stream during the timed steps); `cpu_baseline` times the CPU oracle
-restatement (oracle/cpu_step.py, "port") on the host cores on a bounded sample.
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel: of the 5x5 206->206
+enhance_features_128 convolution's forward, input-gradient and weight-gradient kernels (each
+timed with HIP events around its launches on the launching stream during the timed steps), the
+one with the most time per step; `roofline_kernels` lists all three.  `cpu_baseline` times the
+CPU oracle restatement (oracle/cpu_step.py, "port") on the host cores on a bounded sample.
 """
 import argparse
 import json
@@ -38,6 +39,9 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 / fp16 MFMA (MI355X_MICROARCH.md, chip table; fp32 mode: same denominator)
 PEAK_HBM_GBS = 8000.0
+PROBED = ("fwd", "bwd", "wgrad")
+PASS_KERNEL = {"fwd": "halo_kernel forward", "bwd": "halo_kernel input gradient (masked: act' applied in the halo "
+                                                    "staging)", "wgrad": "wgrad_rh_kernel weight gradient (+ bias)"}
 
 
 def parse():
@@ -115,9 +119,12 @@ def main():
     B = args.batch
     batch = tpgan_train.synthetic_batch(B, dev, seed=1000 + rank, img_size=S)
 
-    # dominant kernel probe: enhance_features_128 (206 -> 206, 5x5, at the full face size) forward
+    # dominant-kernel probes: enhance_features_128 (206 -> 206, 5x5, at the full face size), its
+    # forward, input gradient (the fused backward's first call: masked halo dgrad) and weight
+    # gradient -- the step's three largest kernels; `roofline` reports the one with the most
+    # time per step (profiles/r04/kernel_trace_summary.txt: the weight gradient)
     def match(d, which):
-        return which == "fwd" and d.in_c == 206 and d.out_c == 206 and d.kh == 5 and d.in_h == S
+        return which in PROBED and d.in_c == 206 and d.out_c == 206 and d.kh == 5 and d.in_h == S
 
     # warm-up (autotunes the weight-gradient tiles), one eager step counted for the
     # algorithmic FLOPs, then the step is captured as hipGraph(s)
@@ -178,9 +185,23 @@ def main():
     torch.cuda.synchronize()
     tpgan_ops.PROBE["match"] = None
     evs = tpgan_ops.PROBE["events"]
-    k_ms = sum(ev[0].elapsed_time(ev[1]) for ev in evs) / max(len(evs), 1)
-    k_flops = evs[0][2] if evs else 0
-    achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
+    per = {}
+    for e0, e1, work, which, _ in evs:
+        r = per.setdefault(which, {"ms": 0.0, "n": 0, "flops": work})
+        r["ms"] += e0.elapsed_time(e1)
+        r["n"] += 1
+    n_steps = args.probe_steps if graphed else args.steps
+    kern = []
+    for which, r in per.items():
+        avg = r["ms"] / r["n"]
+        ach = r["flops"] / (avg * 1e-3) / 1e12
+        kern.append({"pass": which, "kernel": PASS_KERNEL.get(which, which), "achieved": round(ach, 2),
+                     "frac": round(ach / PEAK_BF16_TFLOPS, 4), "avg_launch_ms": round(avg, 4), "launches": r["n"],
+                     "ms_per_step": round(r["ms"] / max(n_steps, 1), 4), "flops_per_launch": r["flops"]})
+    kern.sort(key=lambda k: -k["ms_per_step"])
+    top = kern[0] if kern else {"pass": "fwd", "achieved": 0.0, "avg_launch_ms": 0.0, "launches": 0,
+                                "flops_per_launch": 0, "ms_per_step": 0.0}
+    k_ms, k_flops, achieved = top["avg_launch_ms"], top["flops_per_launch"], top["achieved"]
 
     if rank != 0:
         if world > 1:
@@ -206,18 +227,21 @@ def main():
                                "sample": "BASELINE configs[0]: global pathway + D fwd+bwd, B=4, median of %d "
                                          "(%.2f s/step)" % (args.cpu_iters, r["config1_s"])}}
 
-    # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    # HBM bytes per launch of each probed kernel from the committed rocprofv3 PMC passes
     # (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or null
-    traffic, traffic_src = None, None
-    pmc = os.path.join(REPO, "profiles", "pmc_dominant.json")
-    if os.path.exists(pmc) and args.config == 2 and S == 128 and args.dtype == "bf16" and B == 32:
-        with open(pmc) as f:
+    def pmc_traffic(which):
+        path = os.path.join(REPO, "profiles", "pmc_enhance128_%s.json" % which)
+        if not (os.path.exists(path) and args.config == 2 and S == 128 and args.dtype == "bf16" and B == 32):
+            return None, None
+        with open(path) as f:
             pj = json.load(f)
-        traffic = int(pj["traffic_bytes"])
-        traffic_src = ("profiles/pmc_dominant.json: rocprofv3 --pmc FETCH_SIZE (x2, calibrated) + WRITE_SIZE "
-                       "(exact, calibrated), median over the forward-only dispatches (grid filter) of "
-                       "tools/bench_layers.py enhance_128; algorithmic %d B (x, residual in, y out, weights)"
-                       % int(pj.get("algorithmic_bytes", 0)))
+        return int(pj["traffic_bytes"]), (
+            "profiles/pmc_enhance128_%s.json: rocprofv3 --pmc FETCH_SIZE (x2, calibrated) + WRITE_SIZE (exact, "
+            "calibrated), median over that pass's dispatches of tools/bench_layers.py enhance_128; algorithmic %d B"
+            % (which, int(pj.get("algorithmic_bytes", 0))))
+    for k in kern:
+        k["traffic"], _ = pmc_traffic(k["pass"])
+    traffic, traffic_src = pmc_traffic(top["pass"])
     workload = "BASELINE configs[1]: full two-pathway G (global + 4 local) + D train step, 128x128, bf16"
     ext_name = {"resnet50": "ResNet-50", "mobilenetv2": "MobileNetV2"}.get(args.identity)
     if args.config == 5:
@@ -254,11 +278,14 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "tpg halo_kernel fwd, enhance_features_128 (206->206, 5x5, %dx%d, bs%d, +residual, "
-                               "LeakyReLU, %s)" % (S, S, B, args.dtype),
-                     "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4), "launches": len(evs),
+                     "kernel": "tpg %s, enhance_features_128 (206->206, 5x5, %dx%d, bs%d, +residual, LeakyReLU, %s)"
+                               % (PASS_KERNEL.get(top["pass"], top["pass"]), S, S, B, args.dtype),
+                     "pass": top["pass"], "flops_per_launch": k_flops, "avg_launch_ms": round(k_ms, 4),
+                     "launches": top["launches"], "ms_per_step": top["ms_per_step"],
                      "timing": ("HIP events on the launch stream, eager probe steps after the timed graph replays"
-                                if graphed else "HIP events on the launch stream over the timed steps")},
+                                if graphed else "HIP events on the launch stream over the timed steps"),
+                     "selection": "the probed enhance_features_128 kernel with the most time per step"},
+        "roofline_kernels": kern,
         "step_mfma": {"algorithmic_tflop_per_step": round(flops_step / 1e12, 4),
                       "gflop_per_face": round(flops_step / B / 1e9, 2),
                       "achieved_tflops": round(flops_step / (ms_per_step * 1e-3) / 1e12, 2),

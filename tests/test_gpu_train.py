@@ -359,6 +359,54 @@ def test_deterministic_mode_bit_identical(gpu):
         assert torch.equal(a, c)
 
 
+def test_real_ahead_reuse_and_invalidation(gpu, tmp_path):
+    """The next step's precomputed D(real) pass (real_ahead) is used only for the
+    batch it was computed on, unchanged, under the same D weights:
+      - announced and unchanged: reused;
+      - the same batch object refilled in place (copy_) before the step: NOT reused, and the step
+        lands bit for bit where a trainer without real_ahead lands (deterministic mode);
+      - D's weights replaced by load_checkpoint after the pass: NOT reused."""
+    import tpgan_ops
+    import tpgan_train
+    b = tpgan_train.synthetic_batch(4, gpu, seed=23)
+    new_frontal = tpgan_train.synthetic_batch(4, gpu, seed=24)["frontal"]
+    with tpgan_ops.deterministic():
+        G, D = _models(gpu)
+        ref = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False,
+                                       real_ahead=False)
+        ref.step(b)
+        snap = _snapshot(ref)
+        b2 = {k: (v.clone() if k != "frontal" else new_frontal.clone()) for k, v in b.items()}
+        ref.step(b2)
+        torch.cuda.synchronize()
+        want = [t.clone() for t in (ref.fG.data, ref.fD.data)]
+
+        ra = tpgan_train.TPGANTrainer(ref.G, ref.D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16,
+                                      use_dropout=False, real_ahead=True)
+        _restore(ra, snap)
+        bb = {k: v.clone() for k, v in b.items()}
+        ra._real_ahead(bb)  # (as the previous step would have, announcing bb)
+        assert ra._d_real_next is not None
+        bb["frontal"].copy_(new_frontal)  # the caller refills its persistent batch in place
+        ra.step(bb)
+        torch.cuda.synchronize()
+        assert ra.real_ahead_used == 0
+        for a, c in zip(want, (ra.fG.data, ra.fD.data)):
+            assert torch.equal(a, c)
+
+        # unchanged announced batch: reused
+        ra.step(bb, next_b=bb)
+        ra.step(bb)
+        assert ra.real_ahead_used == 1
+        # weights loaded after the pass: the stale pass is dropped
+        ra.save_checkpoint(str(tmp_path), 1)
+        ra.step(bb, next_b=bb)
+        ra.load_checkpoint(str(tmp_path), 1)
+        ra.step(bb)
+        torch.cuda.synchronize()
+        assert ra.real_ahead_used == 1
+
+
 def test_wgrad_side_stream_bit_identical(gpu):
     """Weight gradients on the side stream (tpgan_ops.wgrad_side_stream, TPG_WGRAD_SIDE=1)
     against all of them on the launching stream: deterministic mode, bf16, from the

@@ -110,11 +110,15 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False):
     y = T.new_act(N, Cout, OH, OW, dt, dev)
     res = T.new_act(N, Cout, OH, OW, dt, dev).normal_() if use_res else None
     g = T.new_act(N, Cout, OH, OW, dt, dev).normal_()
+    gy = T.new_act(N, Cout, OH, OW, dt, dev).normal_()
     dx = T.new_act(N, Cin, H, W, dt, dev)
     dw = torch.zeros_like(w)
     d = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
     wd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
-    wd.algo = wg_algo  # (0: the library's untuned default)
+    wd.algo, wd.ksplit = wg_algo  # ((0, 0): the library's untuned default)
+    if wg_algo == (0, 0) and T.AUTOTUNE["cache"]:  # --tune-file: the step's own pick for this shape
+        wd.algo, wd.ksplit = T.AUTOTUNE["cache"].get(T._wgrad_key(wd), (0, 0))
+    gd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)  # fused backward, input gradient only
     wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
     wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
     calls = {
@@ -124,6 +128,10 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False):
                                                        wsd.numel(), stream_ptr())),
         "wgrad": lambda: check(lib.tpg_conv2d_bwd_filter(ctypes.byref(wd), tt(x), tt(g), tt(dw), None, 0,
                                                          stream_ptr())),
+        # the step's fused backward without the weight gradient: g = gy * act'(y) staged in the
+        # input gradient's halo (masked mode) where the geometry allows
+        "bwd": lambda: check(lib.tpg_conv2d_bwd(ctypes.byref(gd), tt(x), tt(w), tt(y), tt(gy), tt(g), tt(dx),
+                                                tt(None), None, wsd.data_ptr(), wsd.numel(), stream_ptr())),
     }
     f = flops(s)
     if sweep:  # every weight-gradient (algo, pixel split) the tuner would try
@@ -160,14 +168,21 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--wg-sweep", action="store_true", help="time every weight-gradient algo / pixel split")
-    ap.add_argument("--wg-algo", default="", help="weight-gradient algo per shape, e.g. enhance_128=12,add_128=7")
+    ap.add_argument("--wg-algo", default="",
+                    help="weight-gradient algo[/pixel splits] per shape, e.g. enhance_128=12/1,add_128=7")
     ap.add_argument("--graph", action="store_true", help="time graph replays (GPU time of short kernels)")
+    ap.add_argument("--tune-file", default=None,
+                    help="weight-gradient picks saved by a train step (bench.py with TPG_TUNE_DUMP=path)")
     a = ap.parse_args()
+    if a.tune_file:
+        T.load_tuning(a.tune_file)
     for name, s in SHAPES.items():
         if a.only and name not in a.only.split(","):
             continue
         algos = dict(kv.split("=") for kv in a.wg_algo.split(",") if kv)
-        run(name, s, a.iters, a.passes.split(","), a.wg_sweep, int(algos.get(name, 0)), a.graph)
+        al = algos.get(name, "0").split("/")
+        run(name, s, a.iters, a.passes.split(","), a.wg_sweep, (int(al[0]), int(al[1]) if len(al) > 1 else 0),
+            a.graph)
 
 
 if __name__ == "__main__":

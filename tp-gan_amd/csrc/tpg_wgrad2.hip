@@ -18,6 +18,12 @@
 #include <type_traits>
 #include <string.h>
 
+// timing ablations (tools only; never in the product build): bit 1 no LDS-DMA, 2 no barrier,
+// 4 no MFMA, 8 no fragment reads, 16 no dW / bias epilogue (accumulators kept live)
+#ifndef TPG_W2_ABL
+#define TPG_W2_ABL 0
+#endif
+
 namespace tpg {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -165,6 +171,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
 
   // DMA of k-tile kt into ring slot `slot` (kt is non-decreasing, +0 or +1 per call)
   auto issue = [&](int kt, int slot) {
+    if constexpr ((TPG_W2_ABL & 1) != 0) return;
     char* st = lds + slot * STAGE;
     const int p0 = pbeg + kt * KP;
     if (fastp) {
@@ -284,6 +291,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
       // alone (bits 0-1 and 3 of the row), so a per-lane base of each fragment plus a constant
       // (lane bases: abase / bbase, computed once per block)
       auto rd = [&](int ks, int r) -> s16x4 {
+        if constexpr ((TPG_W2_ABL & 8) != 0) return s16x4{(short)r, (short)ks, 1, 2};
         if (r < 2 * MREP) return tr_read_o(A + abase[r >> 1], (32 * ks + 4 * (r & 1)) * RBA);
         const int rr = r - 2 * MREP;
         return tr_read_o(B + bbase[rr >> 1], (32 * ks + 4 * (rr & 1)) * RBB);
@@ -311,7 +319,8 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
           const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * n],
                                                                                h[cur][2 * MREP + 2 * n + 1],
                                                                                0, 1, 2, 3, 4, 5, 6, 7));
-          acc[m][n] = mfma16x16x32<DT>(av, bv, acc[m][n]);
+          if constexpr ((TPG_W2_ABL & 4) == 0) acc[m][n] = mfma16x16x32<DT>(av, bv, acc[m][n]);
+          else acc[m][n][0] += (float)av[0] * (float)bv[1];
           if (ks + 1 < NS) {
 #pragma unroll
             for (int r = i * R / M; r < (i + 1) * R / M; ++r) h[cur ^ 1][r] = rd(ks + 1, r);
@@ -366,8 +375,13 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
   };
 
 // k-tile kt+1 retired, the NST-2 k-tiles after it still in flight
+#if (TPG_W2_ABL & 2) != 0
+#define W2_WAIT_BARRIER() \
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"i"((NST - 2) * (GA + GB)) : "memory")
+#else
 #define W2_WAIT_BARRIER() \
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"((NST - 2) * (GA + GB)) : "memory")
+#endif
 
   if (nkt > 0) {
 #pragma unroll
@@ -385,37 +399,95 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
   }
 #undef W2_WAIT_BARRIER
 
-  // ---- epilogue: fp32 atomics into dW (plain read-add-write without a pixel split) (C/D layout: col = lane&15 -> b, row = 4g+reg -> a)
-  const int r_tap = p.tr[tap], s_tap = p.ts[tap];
+  // ---- epilogue: the fp32 tile goes through LDS so that dW is written in whole rows.
+  // The MFMA C layout (col = lane & 15 -> b, row = 4g + reg -> a) made every wave-instruction
+  // touch four 64-byte segments in four dW rows; float atomics of that shape ran at about a
+  // quarter of the full memory-side rate (ablation, profiles/r04/wgrad2_ablation.txt: without
+  // the epilogue enh_8 46 -> 19 us, local_10 40 -> 12 us).  Now:
+  //   sole owner (ksplit == 1): 16-byte read-add-write of 4 consecutive columns per thread;
+  //   pixel split: one no-return atomic per lane, 64 lanes = 64 consecutive columns of ONE row
+  //   (256 contiguous bytes per wave-instruction: the full-rate shape).
+  if (nkt <= 0) return;  // (an empty pixel split adds nothing; block-uniform)
+  if constexpr ((TPG_W2_ABL & 16) != 0) {
+#pragma unroll
+    for (int m = 0; m < MREP; ++m) {
+      asm volatile("" ::"v"(accb[m]));
+#pragma unroll
+      for (int n = 0; n < NREP; ++n) asm volatile("" ::"v"(acc[m][n]));
+    }
+    return;
+  }
+  constexpr int LDC = BN + 4;  // (+4 floats: the g = 0 / 1 row quads of a C write land on disjoint banks)
+  static_assert(BM * LDC * 4 <= NST * STAGE, "C tile fits in the LDS ring");
+  float* Cs = reinterpret_cast<float*>(lds);
+  // every wave's DMAs have landed (the ring's last clamped re-issues included) before it is overwritten
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
   for (int m = 0; m < MREP; ++m)
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int a = a0 + wm * WTM + m * 16 + 4 * g + reg;
-      if (a >= p.Ca) continue;
+    for (int n = 0; n < NREP; ++n)
 #pragma unroll
-      for (int n = 0; n < NREP; ++n) {
-        const int bq = b0 + wn * WTN + n * 16 + l16;
-        int r = r_tap, s = s_tap, b = bq;
-        if constexpr (FLAT) {
-          const int t = bq / p.cbp;
-          b = bq - t * p.cbp;
-          if (t >= p.ntaps || b >= p.Cb) continue;
-          r = p.tr[t];
-          s = p.ts[t];
-        } else if (bq >= p.Cb) {
-          continue;
-        } else if (p.bcomp) {
-          const int rs = bq / p.comp_cb;
-          b = bq - rs * p.comp_cb;
-          r = rs / p.comp_kw;
-          s = rs - r * p.comp_kw;
-        }
-        float* dst = p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss;
-        if (p.ksplit == 1) *dst += acc[m][n][reg];  // sole owner of this dW element
-        else atomicAdd(dst, acc[m][n][reg]);
+      for (int reg = 0; reg < 4; ++reg)
+        Cs[(wm * WTM + m * 16 + 4 * g + reg) * LDC + wn * WTN + n * 16 + l16] = acc[m][n][reg];
+  __syncthreads();
+  const int r_tap = p.tr[tap], s_tap = p.ts[tap];
+  // element offset in dW of tile column col at a = 0; -1: padding column (past Cb or the last tap)
+  auto col_off = [&](int col) -> int {
+    const int bq = b0 + col;
+    int r = r_tap, s = s_tap, b = bq;
+    if constexpr (FLAT) {
+      const int t = bq / p.cbp;
+      b = bq - t * p.cbp;
+      if (t >= p.ntaps || b >= p.Cb) return -1;
+      r = p.tr[t];
+      s = p.ts[t];
+    } else if (bq >= p.Cb) {
+      return -1;
+    } else if (p.bcomp) {
+      const int rs = bq / p.comp_cb;
+      b = bq - rs * p.comp_cb;
+      r = rs / p.comp_kw;
+      s = rs - r * p.comp_kw;
+    }
+    return b * p.w_sb + r * p.w_sr + s * p.w_ss;
+  };
+  const int amax = min(BM, p.Ca - a0);
+  if (p.ksplit == 1) {
+    constexpr int CPR = BN / 4, RPP = 512 / CPR;  // 4-column chunks per row, rows per pass
+    const int ch = tid % CPR, c0 = 4 * ch;
+    int off[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) off[e] = col_off(c0 + e);
+    const bool vec = p.w_sb == 1 && (p.w_sa & 3) == 0 && ((uintptr_t)p.dW & 15) == 0 && off[0] >= 0 &&
+                     (off[0] & 3) == 0 && off[3] == off[0] + 3;
+    for (int row = tid / CPR; row < amax; row += RPP) {
+      const float4 v = *reinterpret_cast<const float4*>(Cs + row * LDC + c0);
+      float* dst = p.dW + (a0 + row) * p.w_sa;
+      if (vec) {
+        float4* d4 = reinterpret_cast<float4*>(dst + off[0]);
+        float4 o = *d4;
+        o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+        *d4 = o;
+      } else {
+        if (off[0] >= 0) dst[off[0]] += v.x;
+        if (off[1] >= 0) dst[off[1]] += v.y;
+        if (off[2] >= 0) dst[off[2]] += v.z;
+        if (off[3] >= 0) dst[off[3]] += v.w;
       }
     }
+  } else {
+    constexpr int CG = BN / 64;  // 64-column groups of a row
+    static_assert(CG * 64 == BN, "row groups");
+    int coff[CG];
+#pragma unroll
+    for (int c = 0; c < CG; ++c) coff[c] = col_off(c * 64 + lane);
+    for (int row = wave; row < amax; row += 8) {
+      float* dst = p.dW + (a0 + row) * p.w_sa;
+#pragma unroll
+      for (int c = 0; c < CG; ++c)
+        if (coff[c] >= 0) atomicAdd(dst + coff[c], Cs[row * LDC + c * 64 + lane]);
+    }
+  }
   if (bias_wave && l16 == 0) {  // every column of accb holds the row sum
 #pragma unroll
     for (int m = 0; m < MREP; ++m)

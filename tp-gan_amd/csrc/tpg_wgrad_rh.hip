@@ -348,24 +348,73 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
 #undef RH_WAIT_BARRIER
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // ---- epilogue: fp32 atomics (plain read-add-write without a pixel split)
+  // ---- epilogue through LDS, in row chunks that fit the ring (see tpg_wgrad2.hip): sole owner
+  // (ksplit == 1) 16-byte read-add-write of 4 consecutive columns; pixel splits one no-return
+  // atomic per lane with 64 lanes on 64 consecutive columns of one dW row (full-rate shape,
+  // instead of the MFMA C layout's four 64-byte segments in four rows)
+  constexpr int LDC = BN + 4;
+  constexpr int RING = 3 * STAGE;
+  constexpr int RCH0 = (RING / (LDC * 4)) / WTM * WTM;  // rows per chunk: whole wave rows
+  constexpr int RCH = RCH0 < BM ? RCH0 : BM;
+  static_assert(RCH >= WTM, "a wave row of the C tile fits in the LDS ring");
+  float* Cs = reinterpret_cast<float*>(lds);
+  const int amax = min(BM, p.Ca - a0);
+  auto col_off = [&](int col) -> int {  // dW element offset of tile column col at a = 0; -1: padding
+    const int tap = col / BC;
+    const int r = r0 + tap / NT, s = s0 + tap % NT, b = b0 + col % BC;
+    if (r >= p.kh || s >= p.kw || b >= p.Cb) return -1;
+    return b * p.w_sb + r * p.w_sr + s * p.w_ss;
+  };
+  constexpr int CG = (BN + 63) / 64;
+  int coff[CG];
 #pragma unroll
-  for (int m = 0; m < MREP; ++m)
+  for (int c = 0; c < CG; ++c) coff[c] = (c * 64 + lane < BN) ? col_off(c * 64 + lane) : -1;
+  const bool vec_base = p.w_sb == 1 && (p.w_sa & 3) == 0 && ((uintptr_t)p.dW & 15) == 0;
+  asm volatile("s_barrier" ::: "memory");  // (every wave's DMAs retired above: the ring is free)
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int a = a0 + wm * WTM + m * 16 + 4 * g + reg;
-      if (a >= p.Ca) continue;
+  for (int c0 = 0; c0 < BM; c0 += RCH) {
+    if (c0 > 0) __syncthreads();  // the previous chunk has been read
+    if (wm * WTM >= c0 && wm * WTM < c0 + RCH) {
 #pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        const int col = wn * WTN + j * 16 + l16;
-        const int tap = col / BC;
-        const int r = r0 + tap / NT, s = s0 + tap % NT, b = b0 + col % BC;
-        if (r >= p.kh || s >= p.kw || b >= p.Cb) continue;
-        float* dst = p.dW + a * p.w_sa + b * p.w_sb + r * p.w_sr + s * p.w_ss;
-        if (p.ksplit == 1) *dst += acc[m][j][reg];
-        else atomicAdd(dst, acc[m][j][reg]);
+      for (int m = 0; m < MREP; ++m)
+#pragma unroll
+        for (int j = 0; j < NREP; ++j)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            Cs[(wm * WTM - c0 + m * 16 + 4 * g + reg) * LDC + wn * WTN + j * 16 + l16] = acc[m][j][reg];
+    }
+    __syncthreads();
+    const int rows = min(RCH, amax - c0);
+    if (p.ksplit == 1) {
+      constexpr int CPR = BN / 4;
+      for (int idx = tid; idx < rows * CPR; idx += 512) {
+        const int row = idx / CPR, cc = 4 * (idx - row * CPR);
+        const float4 v = *reinterpret_cast<const float4*>(Cs + row * LDC + cc);
+        float* dst = p.dW + (a0 + c0 + row) * p.w_sa;
+        const int o0 = col_off(cc);
+        if (vec_base && o0 >= 0 && (o0 & 3) == 0 && col_off(cc + 3) == o0 + 3) {
+          float4* d4 = reinterpret_cast<float4*>(dst + o0);
+          float4 o = *d4;
+          o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+          *d4 = o;
+        } else {
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int oe = col_off(cc + e);
+            if (oe >= 0) dst[oe] += vv[e];
+          }
+        }
+      }
+    } else {
+      for (int row = wave; row < rows; row += 8) {
+        float* dst = p.dW + (a0 + c0 + row) * p.w_sa;
+#pragma unroll
+        for (int c = 0; c < CG; ++c)
+          if (coff[c] >= 0) atomicAdd(dst + coff[c], Cs[row * LDC + c * 64 + lane]);
       }
     }
+  }
   if (bias_wave && l16 == 0) {  // every column of accb holds the row sum
 #pragma unroll
     for (int m = 0; m < MREP; ++m)
