@@ -200,10 +200,13 @@ int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argm
                         tpg_stream_t stream);
 
 /* In-place Adam (torch.optim.Adam semantics, L2 weight_decay added to the gradient) on a
- * flat fp32 buffer (all four pointers 16-byte aligned).  state is a caller-owned device
+ * flat fp32 buffer (the four pointers 4-byte aligned, all at the same offset inside 16 bytes).  state is a caller-owned device
  * float[4] {step, 1 - beta1^step, sqrt(1 - beta2^step), unused}, zero-initialised before the
  * first call: step > 0 sets the step count explicitly, step == 0 advances the device counter
- * by one (what a captured hipGraph replays).  grad_scale multiplies the gradient. */
+ * by one (what a captured hipGraph replays), step < 0 leaves the counter as it is -- a slice of
+ * the buffer updated under the step the last call set (the per-bucket updates of an optimizer
+ * overlapped with the backward: one numel = 0, step = 0 call per step, then one step = -1 call
+ * per bucket).  grad_scale multiplies the gradient. */
 int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  float grad_scale, float* state, tpg_stream_t stream);

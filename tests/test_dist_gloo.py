@@ -130,3 +130,70 @@ def test_overlapped_bucket_sync_gloo_world2():
         assert results[0][1] > 2
         assert same and unhooked
     assert res[0][2] == res[1][2]
+
+
+def _worker_overlap_opt(rank, world, port, q):
+    sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import D_and_G_model as DG
+        import tpgan_ops
+        import tpgan_train
+        torch.manual_seed(5)
+        D = DG.Discriminator()
+        flat = tpgan_train.FlatParams(D, torch.device("cpu"))
+        calls = []
+
+        def opt(off, n):  # the bucket's gradients must already be the reduced ones
+            calls.append((off, n, bool(torch.all(flat.grad[off:off + n] == float(sum(range(1, world + 1)))))))
+
+        sync = tpgan_train.OverlappedGradSync(flat, bucket_mb=2.0, optimizer=opt)
+        results = []
+        for step in range(2):
+            calls.clear()
+            flat.grad.zero_()
+            sync.begin()
+            params = list(D.parameters())
+            order = list(range(len(params))) if rank == 0 else list(reversed(range(len(params))))
+            for i in order:
+                p = params[i]
+                p.grad.fill_(float(rank + 1))
+                if i != 3:
+                    tpgan_ops.GRAD_READY_HOOK[0](p)
+            sync.finish()
+            cover = torch.zeros(flat.grad.numel(), dtype=torch.int32)
+            for off, n, _ in calls:
+                cover[off:off + n] += 1
+            results.append((bool(torch.all(cover == 1)), all(c[2] for c in calls), len(calls), sync.updated))
+        q.put((rank, results))
+    except Exception as e:
+        q.put((rank, [(False, repr(e), 0, False)]))
+        raise
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [1, 2])
+def test_overlapped_optimizer_buckets(world):
+    """OverlappedGradSync(optimizer=...): every element of the flat buffer is handed to the
+    optimizer exactly once per step, bucket by bucket, each bucket only after its all-reduce
+    (world 2: the values seen are the summed ones) -- before and after the step-1 relayout;
+    world 1 runs the same bucketed update with no process group."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlap_opt, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for rank, results in res:
+        for once, reduced, ncalls, updated in results:
+            assert once and reduced and updated, (rank, results)
+            assert ncalls > 2

@@ -312,9 +312,13 @@ def test_prepacked_weights_match_inline_packing(gpu):
     G, D = _models(gpu)
     tr = tpgan_train.TPGANTrainer(G, D, compute_dtype=torch.bfloat16, use_dropout=False)
     b = tpgan_train.synthetic_batch(2, gpu, seed=21)
+    tr.step(b)  # (the first step also re-lays the flat buffers out in gradient-completion order)
     tr.step(b)
     torch.cuda.synchronize()
-    assert len(tr.fG.pack_entries) > 50 and tr.fG.pack_table is not None
+    # images re-packed after the update: one batched table for the whole network, or per bucket
+    # when G's Adam ran bucket by bucket under the backward (TPGANTrainer.overlap_optimizer)
+    assert len(tr.fG.pack_entries) > 50
+    assert tr.fG.pack_table is not None or (tr.overlap_optimizer and tr.fG.range_packs[1])
 
     def run():
         x = b["I128"].clone().requires_grad_(True)
@@ -372,8 +376,10 @@ def test_real_ahead_reuse_and_invalidation(gpu, tmp_path):
     new_frontal = tpgan_train.synthetic_batch(4, gpu, seed=24)["frontal"]
     with tpgan_ops.deterministic():
         G, D = _models(gpu)
+        # (both trainers keep the module-order flat layout -- no bucketed optimizer, hence no step-1
+        # relayout at world 1 -- so that one's snapshot restores into the other)
         ref = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False,
-                                       real_ahead=False)
+                                       real_ahead=False, overlap_optimizer=False)
         ref.step(b)
         snap = _snapshot(ref)
         b2 = {k: (v.clone() if k != "frontal" else new_frontal.clone()) for k, v in b.items()}
@@ -382,7 +388,7 @@ def test_real_ahead_reuse_and_invalidation(gpu, tmp_path):
         want = [t.clone() for t in (ref.fG.data, ref.fD.data)]
 
         ra = tpgan_train.TPGANTrainer(ref.G, ref.D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16,
-                                      use_dropout=False, real_ahead=True)
+                                      use_dropout=False, real_ahead=True, overlap_optimizer=False)
         _restore(ra, snap)
         bb = {k: v.clone() for k, v in b.items()}
         ra._real_ahead(bb)  # (as the previous step would have, announcing bb)
@@ -405,6 +411,41 @@ def test_real_ahead_reuse_and_invalidation(gpu, tmp_path):
         ra.step(bb)
         torch.cuda.synchronize()
         assert ra.real_ahead_used == 1
+
+
+def test_bucketed_optimizer_bit_identical(gpu):
+    """TPGANTrainer(overlap_optimizer=True): G's Adam and weight repack issued bucket by bucket
+    on the communication stream under the G backward (world 1) land bit for bit where the
+    whole-network update after the backward lands (deterministic mode, bf16, same state; the
+    Adam kernel's update of an element must not depend on where its bucket slice starts)."""
+    import tpgan_ops
+    import tpgan_train
+    G, D = _models(gpu)
+    tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False,
+                                  overlap_optimizer=True)
+    assert tr.gsync is not None and tr.gsync.optimizer is not None
+    b = tpgan_train.synthetic_batch(4, gpu, seed=29)
+    with tpgan_ops.deterministic():
+        tr.step(b)  # (learns the bucket layout and relays the flat buffers out)
+        torch.cuda.synchronize()
+        snap = _snapshot(tr)
+        res = {}
+        for mode in ("bucketed", "whole", "bucketed"):
+            _restore(tr, snap)
+            opt = tr.gsync.optimizer
+            if mode == "whole":
+                tr.gsync.optimizer = None
+            try:
+                tr.step(b)
+                tr.step(b)
+            finally:
+                tr.gsync.optimizer = opt
+            torch.cuda.synchronize()
+            res.setdefault(mode, []).append([t.clone() for t in (tr.fG.data, tr.fG.exp_avg, tr.fG.exp_avg_sq,
+                                                                 tr.fG.adam_state, tr.fD.data)])
+    for a, c, a2 in zip(res["bucketed"][0], res["whole"][0], res["bucketed"][1]):
+        assert torch.equal(a, a2)
+        assert torch.equal(a, c)
 
 
 def test_wgrad_side_stream_bit_identical(gpu):

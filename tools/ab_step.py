@@ -1,0 +1,108 @@
+"""Interleaved A/B of tpgan_ops / tpgan_train module switches on the real train step (one
+process, one trainer, variants alternated round by round: cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/ab_step.py [--steps 10] [--rounds 5] VARIANT [VARIANT ...]
+
+VARIANT = name[:module.ATTR[.key]=value,...], e.g.
+    base   side:tpgan_ops.WGRAD_SIDE.enabled=1   nogroup:tpgan_ops.GROUP.enabled=0
+Values are parsed as int / float / bool literals.  Prints per-variant median and min ms/step.
+"""
+import argparse
+import importlib
+import os
+import statistics
+import sys
+import time
+
+TRAINER = [None]  # "trainer.ATTR=value" sets an attribute of the trainer (e.g. trainer.real_ahead=1)
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "tp-gan_amd")]
+
+import torch  # noqa: E402
+
+
+def parse_variant(spec):
+    name, _, rest = spec.partition(":")
+    sets = []
+    for kv in filter(None, rest.split(",")):
+        path, _, val = kv.partition("=")
+        parts = path.split(".")
+        mod = TRAINER if parts[0] == "trainer" else importlib.import_module(parts[0])
+        lv = val.lower()
+        if lv in ("true", "false", "none"):
+            v = {"true": True, "false": False, "none": None}[lv]
+        else:
+            v = float(val) if "." in val else int(val)
+        sets.append((mod, parts[1:], v))
+    return name, sets
+
+
+def apply(sets):
+    old = []
+    for mod, attrs, v in sets:
+        obj = TRAINER[0] if mod is TRAINER else mod
+        for a in attrs[:-1]:
+            obj = getattr(obj, a) if not isinstance(obj, dict) else obj[a]
+        last = attrs[-1]
+        if isinstance(obj, dict):
+            old.append((obj, last, obj[last], True))
+            obj[last] = type(obj[last])(v) if isinstance(obj[last], (bool, int, float)) else v
+        else:
+            old.append((obj, last, getattr(obj, last), False))
+            setattr(obj, last, v)
+    return old
+
+
+def restore(old):
+    for obj, last, v, is_dict in reversed(old):
+        if is_dict:
+            obj[last] = v
+        else:
+            setattr(obj, last, v)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    a = ap.parse_args()
+    import D_and_G_model as DG
+    import tpgan_train
+    from config import G as GCFG
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    G = DG.Generator(GCFG["zdim"], GCFG["num_classes"], use_batchnorm=False).to(dev)
+    D = DG.Discriminator().to(dev)
+    tr = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16)
+    TRAINER[0] = tr
+    b = tpgan_train.synthetic_batch(a.batch, dev, seed=1000)
+    variants = [parse_variant(v) for v in a.variants]  # (after TRAINER is set)
+    for name, sets in variants:  # warm-up under every variant (autotuning, first-use packing)
+        old = apply(sets)
+        for _ in range(a.warmup):
+            tr.step(b, next_b=b)
+        restore(old)
+    torch.cuda.synchronize()
+    res = {name: [] for name, _ in variants}
+    for r in range(a.rounds):
+        for name, sets in variants:
+            old = apply(sets)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                tr.step(b, next_b=b)
+            torch.cuda.synchronize()
+            res[name].append((time.perf_counter() - t0) / a.steps * 1e3)
+            restore(old)
+        print("round %d: %s" % (r, "  ".join("%s %.3f" % (n, res[n][-1]) for n, _ in variants)), flush=True)
+    for name, _ in variants:
+        v = res[name]
+        print("%-12s median %.3f ms/step  min %.3f  (%s)" % (name, statistics.median(v), min(v),
+                                                          " ".join("%.2f" % x for x in v)))
+
+
+if __name__ == "__main__":
+    main()

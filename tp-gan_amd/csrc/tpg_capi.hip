@@ -479,7 +479,7 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   else if (a.Nout <= 80) bn = 80;
   else if (a.Nout <= 96) bn = 96;
   else if (a.Nout <= 128) bn = 128;
-  else if (a.Nout > 192 && a.Nout <= 208) bn = 208;
+  else if (a.Nout > 192 && a.Nout <= 208) bn = 208;  // (BN 224 on 4 x 2 waves measured 2 % slower, r04)
   else {
     // fewest padded columns among the 128 / 192 / 224 tiles, the wider tile on ties
     // (measured: enhance_16 768->768 at 16x16 -24 %, the 8x8 576-channel layers +6 µs)
@@ -1362,12 +1362,13 @@ extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, floa
                             float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                             float grad_scale, float* state, tpg_stream_t stream) {
   TPG_GROUP_SYNC();
-  if (numel == 0) return 0;
-  if (!param || !grad || !exp_avg || !exp_avg_sq || !state) return fail(-10, "adam: NULL pointer");
-  if (step < 0) return fail(-2, "adam: step must be >= 0");
+  if (numel < 0) return fail(-2, "adam: numel must be >= 0");
+  if (numel == 0 && step < 0) return 0;
+  if (!state) return fail(-10, "adam: NULL state");
+  if (numel > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) return fail(-10, "adam: NULL pointer");
   const int rc = tpg_adam_impl(numel, param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step,
                                grad_scale, state, (hipStream_t)stream);
-  if (rc == -1) return fail(-15, "adam: buffers must be 16-byte aligned");
+  if (rc == -1) return fail(-15, "adam: buffers must be 4-byte aligned, at one offset inside 16 bytes");
   return hip_check(rc, "adam");
 }
 

@@ -538,37 +538,71 @@ __global__ void adam_sched_kernel(float* st, float b1, float b2, int32_t host_st
   st[2] = sqrtf(1.f - powf(b2, t));
 }
 
-__device__ __forceinline__ void adam_one(float& pv, float g, float& mv, float& vv, float lr_bc1, float b1, float b2,
-                                         float eps, float wd, float bc2s) {
+// (no FP contraction: the compiler fused differently in the scalar head, the unrolled body and
+// the remainder loop, so an element's update depended by an ulp on where its bucket slice started)
+__device__ __forceinline__ void adam_one(float& pv, float g, float gscale, float& mv, float& vv, float lr_bc1, float b1,
+                                         float b2, float eps, float wd, float bc2s) {
+#pragma clang fp contract(off)
+  g *= gscale;
   if (wd != 0.f) g += wd * pv;
   mv = b1 * mv + (1.f - b1) * g;
   vv = b2 * vv + (1.f - b2) * g * g;
   pv = pv - lr_bc1 * mv / (sqrtf(vv) / bc2s + eps);
 }
 
+// head: elements before the first 16-byte boundary (a bucket slice of the flat buffers starts
+// wherever its first parameter does; all four buffers share the misalignment), updated one per
+// thread by block 0; the rest from p + head on in float4s
 __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ gr,
                                                    float* __restrict__ m, float* __restrict__ v, float lr, float b1,
                                                    float b2, float eps, float wd, const float* __restrict__ st,
-                                                   float gscale) {
+                                                   float gscale, int head) {
   if (st[3] != 0.f) return;  // non-finite gradients this step (grad_finite_kernel)
   const float lr_bc1 = lr / st[1], bc2s = st[2];
+  if (head > 0) {
+    if (blockIdx.x == 0 && (int)threadIdx.x < head)
+      adam_one(p[threadIdx.x], gr[threadIdx.x], gscale, m[threadIdx.x], v[threadIdx.x], lr_bc1, b1, b2, eps, wd, bc2s);
+    p += head; gr += head; m += head; v += head; n -= head;
+  }
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+  // two float4 of each operand per thread and iteration: eight 16-byte loads in flight
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    float4 pv[2], g[2], mv[2], vv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      pv[u] = reinterpret_cast<float4*>(p)[i + u * stride];
+      g[u] = reinterpret_cast<const float4*>(gr)[i + u * stride];
+      mv[u] = reinterpret_cast<float4*>(m)[i + u * stride];
+      vv[u] = reinterpret_cast<float4*>(v)[i + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      adam_one(pv[u].x, g[u].x, gscale, mv[u].x, vv[u].x, lr_bc1, b1, b2, eps, wd, bc2s);
+      adam_one(pv[u].y, g[u].y, gscale, mv[u].y, vv[u].y, lr_bc1, b1, b2, eps, wd, bc2s);
+      adam_one(pv[u].z, g[u].z, gscale, mv[u].z, vv[u].z, lr_bc1, b1, b2, eps, wd, bc2s);
+      adam_one(pv[u].w, g[u].w, gscale, mv[u].w, vv[u].w, lr_bc1, b1, b2, eps, wd, bc2s);
+      reinterpret_cast<float4*>(p)[i + u * stride] = pv[u];
+      reinterpret_cast<float4*>(m)[i + u * stride] = mv[u];
+      reinterpret_cast<float4*>(v)[i + u * stride] = vv[u];
+    }
+  }
+  for (; i < n4; i += stride) {
     float4 pv = reinterpret_cast<float4*>(p)[i];
     const float4 g = reinterpret_cast<const float4*>(gr)[i];
     float4 mv = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam_one(pv.x, g.x * gscale, mv.x, vv.x, lr_bc1, b1, b2, eps, wd, bc2s);
-    adam_one(pv.y, g.y * gscale, mv.y, vv.y, lr_bc1, b1, b2, eps, wd, bc2s);
-    adam_one(pv.z, g.z * gscale, mv.z, vv.z, lr_bc1, b1, b2, eps, wd, bc2s);
-    adam_one(pv.w, g.w * gscale, mv.w, vv.w, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.x, g.x, gscale, mv.x, vv.x, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.y, g.y, gscale, mv.y, vv.y, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.z, g.z, gscale, mv.z, vv.z, lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(pv.w, g.w, gscale, mv.w, vv.w, lr_bc1, b1, b2, eps, wd, bc2s);
     reinterpret_cast<float4*>(p)[i] = pv;
     reinterpret_cast<float4*>(m)[i] = mv;
     reinterpret_cast<float4*>(v)[i] = vv;
   }
   for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
-    adam_one(p[i], gr[i] * gscale, m[i], v[i], lr_bc1, b1, b2, eps, wd, bc2s);
+    adam_one(p[i], gr[i], gscale, m[i], v[i], lr_bc1, b1, b2, eps, wd, bc2s);
 }
 
 // st[3] := 1 when any gradient element is inf / NaN (st[3] zeroed by a memset node first; every
@@ -762,13 +796,17 @@ extern "C" int32_t tpg_adam_impl(int64_t numel, float* param, const float* grad,
                                   float b1, float b2, float eps, float wd, int32_t host_step, float gscale,
                                   float* state, hipStream_t s) {
   // argument checks before any launch: an error must not advance the device step counter
-  const bool vec = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
-  if (!vec) return -1;
-  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, state, b1, b2, host_step);
-  int blocks = (int)std::min<int64_t>((numel / 4 + 255) / 256, 4096);
+  // the four buffers must share their offset inside a 16-byte chunk (elements of one flat layout)
+  const uintptr_t mis = (uintptr_t)param % 16;
+  if ((uintptr_t)param % 4 || (uintptr_t)grad % 16 != mis || (uintptr_t)m % 16 != mis || (uintptr_t)v % 16 != mis)
+    return -1;
+  if (host_step >= 0) hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, state, b1, b2, host_step);
+  if (numel <= 0) return (int)hipGetLastError();
+  const int head = (int)std::min<int64_t>(numel, mis ? (int64_t)((16 - mis) / 4) : 0);
+  int blocks = (int)std::min<int64_t>(((numel - head) / 4 + 255) / 256, 4096);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, state,
-                     gscale);
+                     gscale, head);
   return (int)hipGetLastError();
 }
 

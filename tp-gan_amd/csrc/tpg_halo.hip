@@ -87,6 +87,11 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
   return a.u;
 }
 
+// (A/B builds: -DTPG_HALO_ROWMAJOR=1 restores the row-major dispatch order of the tiles)
+#ifndef TPG_HALO_ROWMAJOR
+#define TPG_HALO_ROWMAJOR 0
+#endif
+
 template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
 __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> GA) {
   // block -> (member, x = sub-tile group, y = N-tile, z = k split); a grouped grid is 1-D in
@@ -105,6 +110,22 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     by = yz - bz * q.ntiles;
   }
   const HaloArgs& p = GA.a[mem];
+  if constexpr (NG == 1 && !TPG_HALO_ROWMAJOR) {
+    // XCD-aware sub-tile order (one image tile per block, >= 64 blocks): physical block b runs on
+    // XCD b % 8, so each XCD gets a contiguous range of logical tiles, and logical tiles walk DOWN
+    // the tile columns of an image -- vertically adjacent tiles, which share k - 1 rows of their
+    // input halo (a third of an 8 x 32 tile's 12 x 36 halo at k = 5), then run together on one
+    // XCD and meet in its L2 instead of being re-read from HBM by another XCD
+    const int nbx = gridDim.x;
+    if (p.IMG == 1 && nbx >= 64 && nbx == p.N * p.tiles_h * p.tiles_w) {
+      const int full = nbx & ~7;
+      const int L = bx < full ? (bx & 7) * (full >> 3) + (bx >> 3) : bx;
+      const int tiles = p.tiles_h * p.tiles_w;
+      const int img = L / tiles, r = L - img * tiles;
+      const int tx = r / p.tiles_h, ty = r - tx * p.tiles_h;
+      bx = img * tiles + ty * p.tiles_w + tx;
+    }
+  }
   using E = dt_t<DT>;
   constexpr bool BF = DT != 0;  // 16-bit operands (bf16 or fp16)
   constexpr int EPC = 16 / sizeof(E);       // elements per 16-byte chunk

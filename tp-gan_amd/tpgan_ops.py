@@ -438,7 +438,8 @@ def _pack_entry(flat, key, d, op, w):
     e.dev = torch.frombuffer(bytearray(single.raw), dtype=torch.uint8).to(w.device)
     e.epoch = -1
     flat.pack_entries[key] = e
-    flat.pack_table = None  # the batched table must be rebuilt
+    flat.pack_table = None  # the batched tables must be rebuilt
+    flat.pack_version = getattr(flat, "pack_version", 0) + 1
     return e
 
 
@@ -1343,6 +1344,50 @@ def maxout2(x):
 def grad_check(grad, state):
     """state[3] := 1 if grad holds an inf / NaN (the next adam_step on `state` then skips)."""
     check(load().tpg_grad_check(grad.numel(), grad.data_ptr(), state.data_ptr(), stream_ptr()))
+
+
+def adam_advance(state, beta1, beta2):
+    """Advance the device step counter in `state` (and its bias corrections) without updating
+    anything: the per-step call of an optimizer whose buckets then run adam_slice."""
+    lib = load()
+    check(lib.tpg_adam(0, None, None, None, None, 0.0, beta1, beta2, 0.0, 0.0, 0, 1.0, state.data_ptr(),
+                       stream_ptr()))
+
+
+def adam_slice(param, grad, exp_avg, exp_avg_sq, off, n, lr, beta1, beta2, eps, weight_decay, state, grad_scale=1.0):
+    """Adam on elements [off, off + n) of the flat buffers under the step adam_advance set."""
+    lib = load()
+    check(lib.tpg_adam(n, param.data_ptr() + 4 * off, grad.data_ptr() + 4 * off, exp_avg.data_ptr() + 4 * off,
+                       exp_avg_sq.data_ptr() + 4 * off, lr, beta1, beta2, eps, weight_decay, -1, grad_scale,
+                       state.data_ptr(), stream_ptr()))
+
+
+def repack_range(flat, off, n, epoch):
+    """Re-pack, in one launch on the current stream, the weight images of the parameters that
+    lie in elements [off, off + n) of flat.data, marking them packed at `epoch`."""
+    cache = getattr(flat, "range_packs", None)
+    if cache is None or cache[0] != flat.pack_version:
+        cache = flat.range_packs = (flat.pack_version, {})
+    hit = cache[1].get((off, n))
+    lib = load()
+    if hit is None:
+        base = flat.data.data_ptr()
+        entries = [e for k, e in flat.pack_entries.items()
+                   if e is not None and e.njobs and off <= (k[2] - base) // 4 < off + n]
+        if entries:
+            raw = b"".join(e.jobs for e in entries)
+            nj = sum(e.njobs for e in entries)
+            host = ctypes.create_string_buffer(raw, len(raw))
+            nblocks = lib.tpg_pack_prepare(host, nj)
+            hit = (entries, torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(flat.data.device), nj, nblocks)
+        else:
+            hit = (entries, None, 0, 0)
+        cache[1][(off, n)] = hit
+    entries, dev, nj, nblocks = hit
+    if nj:
+        check(lib.tpg_pack_run(dev.data_ptr(), nj, nblocks, stream_ptr()))
+    for e in entries:
+        e.epoch = epoch
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, state, step=0, grad_scale=1.0):

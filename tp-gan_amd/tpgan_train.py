@@ -20,7 +20,9 @@ Parameters of G and D live in one flat fp32 buffer each (params are views), so t
 optimizer is one HIP Adam launch per network and the data-parallel exchange is one
 RCCL all-reduce per network (torch.distributed, backend "nccl" = RCCL over xGMI).
 """
+import gc
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -48,6 +50,7 @@ class FlatParams:
         self.layout_version = 0   # bumped by relayout(): captured hipGraphs hold the old buffers
         self.pack_entries = {}    # tpgan_ops pre-packed weight images of this network's convs
         self.pack_table = None
+        self.pack_version = 0     # bumped whenever pack_entries change (per-bucket pack tables follow it)
         self.offsets = []
         off = 0
         for p in self.params:
@@ -76,6 +79,7 @@ class FlatParams:
         self.layout_version += 1
         self.pack_entries = {}  # weights moved: packed images are rebuilt on next use
         self.pack_table = None
+        self.pack_version += 1
         for i, p in enumerate(self.params):
             n = p.numel()
             p.data = self._view(self.data, p, offsets[i], n)
@@ -119,6 +123,21 @@ class FlatParams:
         drives Adam's bias correction is adam_state[0], which a skipped update leaves alone
         (self.step counts adam() calls, skipped or not)."""
         return int(self.skipped.item())
+
+    # ---- the same update bucket by bucket (OverlappedGradSync's optimizer): adam_begin once per
+    # step on the launching stream, adam_bucket per bucket on the communication stream as its
+    # gradients complete (under the rest of the backward), adam_end when all have been issued.
+    def adam_begin(self, betas=(0.5, 0.999)):
+        self.step += 1
+        tpgan_ops.adam_advance(self.adam_state, betas[0], betas[1])
+
+    def adam_bucket(self, off, n, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0):
+        tpgan_ops.adam_slice(self.data, self.grad, self.exp_avg, self.exp_avg_sq, off, n, lr, betas[0], betas[1], eps,
+                             weight_decay, self.adam_state, grad_scale)
+        tpgan_ops.repack_range(self, off, n, self.epoch + 1)  # (the images of these parameters, at the new epoch)
+
+    def adam_end(self):
+        self.epoch += 1  # (images outside every bucket range keep the old epoch: re-packed on next use)
 
     def last_step_skipped(self):
         """True when the last adam(check_finite=True) found non-finite gradients (synchronises)."""
@@ -229,9 +248,14 @@ class OverlappedGradSync(GradSync):
     their gradients completing (broadcast, so all ranks agree), which turns "bucket k is
     ready" into "the k-th stretch of the backward is done" — DDP's bucket rebuild."""
 
-    def __init__(self, flat, group=None, bucket_mb=32.0, count_accumulate=False):
+    def __init__(self, flat, group=None, bucket_mb=32.0, count_accumulate=False, optimizer=None):
         super(OverlappedGradSync, self).__init__(group)
         self.flat = flat
+        # optimizer(off, n): enqueue the update of flat[off:off + n] on the current stream; each
+        # bucket's update runs on the communication stream right behind its all-reduce (world 1:
+        # behind its producers' events), i.e. under the remaining backward
+        self.optimizer = optimizer
+        self.updated = False  # set by finish(): this step's update was issued bucket by bucket
         self.bucket_bytes = int(bucket_mb * 2 ** 20)
         self.active = False
         self.order_learned = False
@@ -274,9 +298,10 @@ class OverlappedGradSync(GradSync):
                 self.bucket_of[i] = b
 
     def begin(self):
-        if self.world == 1:
+        if self.world == 1 and self.optimizer is None:
             return
         self.active = True
+        self.updated = False
         if self.expected is not None:  # parameters that get no gradient at all count as done
             self.pending = [sum(1 for i in idxs if self.expected[i] > 0) for idxs in self.buckets]
         else:
@@ -332,9 +357,20 @@ class OverlappedGradSync(GradSync):
                     self.comm.wait_event(ev)
                 if after_stream is not None:
                     self.comm.wait_stream(after_stream)
-                self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+                if self.world > 1:
+                    w = dist.all_reduce(view, group=self.group, async_op=True)
+                    self.works.append(w)
+                    if self.optimizer is not None:
+                        w.wait()  # (the communication stream waits for the collective)
+                if self.optimizer is not None:
+                    self.optimizer(off, n)
         else:
-            self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+            if self.world > 1:
+                self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+            if self.optimizer is not None:
+                if self.works:
+                    self.works[-1].wait()
+                self.optimizer(off, n)
 
     def finish(self):
         if not self.active:
@@ -360,6 +396,10 @@ class OverlappedGradSync(GradSync):
         for w in self.works:
             w.wait()
         self.works = []
+        if self.optimizer is not None:
+            if cur is not None:
+                cur.wait_stream(self.comm)
+            self.updated = True
         if not self.order_learned:
             self._learn_order()
 
@@ -371,7 +411,8 @@ class OverlappedGradSync(GradSync):
         seen = set(self.order)
         order = list(self.order) + [i for i in reversed(range(n)) if i not in seen]
         t = torch.tensor(order, dtype=torch.int64, device=f.grad.device)
-        dist.broadcast(t, 0, group=self.group)
+        if self.world > 1:
+            dist.broadcast(t, 0, group=self.group)
         # layout: the first-completed parameters at the END of the buffer, so that the
         # reverse-order bucketing of _build() follows the completion order
         f.relayout([int(i) for i in reversed(t.tolist())])
@@ -382,6 +423,16 @@ class OverlappedGradSync(GradSync):
         if self.active:  # already being reduced bucket by bucket
             return self.finish()
         return super(OverlappedGradSync, self).allreduce(flat)
+
+
+def _weak_method(m):
+    ref = weakref.WeakMethod(m)
+
+    def call(*args):
+        f = ref()
+        if f is not None:
+            f(*args)
+    return call
 
 
 def _hp_equal(a, b):
@@ -404,7 +455,7 @@ class TPGANTrainer:
 
     def __init__(self, G, D, lr=1e-4, betas=(0.5, 0.999), compute_dtype=torch.bfloat16, loss_weights=None,
                  gradient_penalty=False, process_group=None, identity_fn=None, use_dropout=True, overlap=True,
-                 bucket_mb=32.0, loss_scale=None, real_ahead=None):
+                 bucket_mb=32.0, loss_scale=None, real_ahead=None, overlap_optimizer=None):
         self.G, self.D = G, D
         # fp16 activations / gradients (BASELINE configs[4]): a static loss scale keeps the
         # per-element image gradients (~1/(B*3*H*W)) out of fp16's subnormal range; the scale
@@ -426,7 +477,22 @@ class TPGANTrainer:
         self.world = self.sync.world
         # G's 551 MB of gradients are reduced bucket by bucket during the G backward, D's 54 MB
         # during the D-step backward (buckets of bucket_mb / 4: D's backward is ~5x shorter)
-        self.gsync = OverlappedGradSync(self.fG, process_group, bucket_mb) if (overlap and self.world > 1) else None
+        # overlap_optimizer: G's Adam (and the repack of its bf16 weight images) bucket by bucket
+        # on the communication stream as each bucket's gradients complete (world > 1: right behind
+        # its all-reduce), under the rest of the G backward; never with a loss scale (the fp16
+        # step's overflow check must see every gradient before any update).  Off by default:
+        # measured 35.14 vs 33.27 ms/step at world 1 (tools/ab_step.py, interleaved rounds,
+        # profiles/r04/ab_bucketed_adam.txt) -- the full-chip Adam / pack grids on the second
+        # stream slow the backward's kernels more than the ~0.7 ms of update they hide
+        if overlap_optimizer is None:
+            overlap_optimizer = False
+        self.overlap_optimizer = bool(overlap_optimizer) and self.loss_scale == 1.0
+        # (a weak reference: a bound method would make trainer <-> gsync a reference cycle, so a
+        # dropped trainer's GPU buffers would wait for the cyclic GC -- which may then run in the
+        # middle of another trainer's graph capture and free memory there)
+        g_opt = _weak_method(self._g_bucket_update) if self.overlap_optimizer else None
+        self.gsync = (OverlappedGradSync(self.fG, process_group, bucket_mb, optimizer=g_opt)
+                      if (overlap and (self.world > 1 or g_opt is not None)) else None)
         # (with WGAN-GP a D parameter gets a second gradient contribution from the double
         # backward, after its first one: D's buckets then wait for the contribution count the
         # first step observed, OverlappedGradSync(count_accumulate=True))
@@ -443,6 +509,9 @@ class TPGANTrainer:
         self.identity_fn = identity_fn
         self.sync.broadcast(self.fG)
         self.sync.broadcast(self.fD)
+
+    def _g_bucket_update(self, off, n):
+        self.fG.adam_bucket(off, n, self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale)
 
     def _allreduce(self, flat):
         ov = self.gsync if flat is self.fG else self.dsync
@@ -563,6 +632,8 @@ class TPGANTrainer:
                 l_ip = self.identity_fn(f32, front)
             loss_G = loss_G + w["weight_identity_preserving"] * l_ip
         if self.gsync is not None and not self._capturing:
+            if self.gsync.optimizer is not None:
+                self.fG.adam_begin(self.betas)  # (the step counter, once, ahead of every bucket's update)
             self.gsync.begin()
         with tpgan_ops.roctx_range("G-bwd"), tpgan_ops.wgrad_side_stream():
             (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
@@ -586,8 +657,12 @@ class TPGANTrainer:
 
     def _phase_c(self, b):
         with tpgan_ops.roctx_range("G-adam"):
-            self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
-                         check_finite=self.loss_scale != 1.0)
+            if self.gsync is not None and self.gsync.updated:
+                self.gsync.updated = False  # (updated bucket by bucket under the G backward)
+                self.fG.adam_end()
+            else:
+                self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
+                             check_finite=self.loss_scale != 1.0)
         out = {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
         if self.loss_scale != 1.0:  # device tensors: reading them is the caller's synchronisation
             out["skipped_D"], out["skipped_G"] = self.fD.skipped, self.fG.skipped
@@ -698,6 +773,7 @@ class TPGANTrainer:
         capture requires."""
         self._static = {k: v.clone() for k, v in b.items()}
         self._d_real_next = None  # (graph replays never run the eager real_ahead pass)
+        gc.collect()  # (nothing of earlier steps or trainers may be freed while a graph is being captured)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         # the data-parallel bucket layout is re-learned after the first overlapped step
@@ -711,6 +787,12 @@ class TPGANTrainer:
         torch.cuda.synchronize()
         if segmented is None:
             segmented = self.world > 1
+        # the captured phase C repacks every weight image with one batched launch, whose job table
+        # is built (host -> device copy) on first use: build it now, outside the capture (the eager
+        # steps updated G bucket by bucket and never needed it); the images are re-packed unchanged
+        tpgan_ops.repack(self.fG)
+        tpgan_ops.repack(self.fD)
+        torch.cuda.synchronize()
         self._capturing = True  # graph replays reduce G in one call between phases
         self._segmented = bool(segmented)
         phases = (self._phase_a, self._phase_b, self._phase_c)
