@@ -42,6 +42,13 @@ def test_bench_torchrun_two_ranks_one_gpu(gpu):
     assert out["n_gpus"] == 2 and out["steps"] == 2 and out["scaling"] == "weak"
     assert out["config"]["global_batch"] == 4 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and out["ms_per_step"] > 0
+    # the roofline object names the probed enhance_features_128 kernel with the most time per step,
+    # and the forward / input-gradient / weight-gradient probes are all listed
+    kern = out["roofline_kernels"]
+    assert sorted(k["pass"] for k in kern) == ["bwd", "fwd", "wgrad"], kern
+    assert out["roofline"]["pass"] == kern[0]["pass"]
+    assert kern[0]["ms_per_step"] == max(k["ms_per_step"] for k in kern)
+    assert all(0 < k["frac"] < 1 for k in kern), kern
     dp = out["dp"]
     assert dp["backend"] == "gloo"
     # every step after the first reuses the D(real) pass the previous one ran under G's tail

@@ -92,6 +92,7 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
 #define TPG_HALO_ROWMAJOR 0
 #endif
 
+
 template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
 __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> GA) {
   // block -> (member, x = sub-tile group, y = N-tile, z = k split); a grouped grid is 1-D in
@@ -388,10 +389,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   };
 
   // Software pipeline over steps s = ks*ntaps + t, one barrier per step:
-  //   start of s : LDS-DMA of step s+2's weights into ring slot (s+2)%3 (unconditional,
-  //                clamped, so every wave always has GL DMA pieces per step in flight);
-  //                at t == 0 the halo of k-step ks+1 into registers
-  //   body       : MFMAs on ring slot s%3 and halo buffer ks&1
+  //   start of s : at t == 0 the halo of k-step ks+1 into registers
+  //   body       : MFMAs on ring slot s%3 and halo buffer ks&1, then the LDS-DMA of step s+2's
+  //                weights into ring slot (s+2)%3 (unconditional, clamped, so every wave
+  //                always has GL DMA pieces per step in flight)
   //   end of s   : at t == ntaps-1 write the next halo to LDS; s_waitcnt vmcnt(GL)
   //                retires step s+1's DMA (issued during s-1) while step s+2's stays in
   //                flight; lgkmcnt(0); s_barrier.  Step s+1 then reads what was retired.
@@ -418,9 +419,12 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         }
       }
       const int slot2 = slot == 0 ? 2 : slot - 1;  // (s + 2) % 3
-      issue_w(min(s + 2, total - 1), slot2);
       const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];  // read ahead of its use
       compute(ks & 1, slot, toff);
+      // step s+2's weight DMA behind this step's fragment reads and MFMAs (it has until the end of
+      // step s+1): issued ahead of them it delayed the reads the first MFMAs wait on -- 1-3.5 %
+      // per layer (r04: enhance_128 fwd 1.153 -> 1.142 ms, add_128 0.416 -> 0.401)
+      issue_w(min(s + 2, total - 1), slot2);
       toff = toff_next;
       if (t == ntaps - 1 && more_ks) store_halo((ks + 1) & 1);
       if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
