@@ -22,10 +22,15 @@ import torch  # noqa: E402
 
 
 def parse_variant(spec):
+    """-> (name, settings, stream priority or None)."""
     name, _, rest = spec.partition(":")
     sets = []
+    prio = None
     for kv in filter(None, rest.split(",")):
         path, _, val = kv.partition("=")
+        if path == "stream.priority":  # the step itself runs on a stream of this priority
+            prio = int(val)
+            continue
         parts = path.split(".")
         mod = TRAINER if parts[0] == "trainer" else importlib.import_module(parts[0])
         lv = val.lower()
@@ -34,7 +39,7 @@ def parse_variant(spec):
         else:
             v = float(val) if "." in val else int(val)
         sets.append((mod, parts[1:], v))
-    return name, sets
+    return name, sets, prio
 
 
 def apply(sets):
@@ -68,6 +73,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--identity", default="none", choices=["none", "resnet50", "mobilenetv2"])
+    ap.add_argument("--gp", action="store_true")
     a = ap.parse_args()
     import D_and_G_model as DG
     import tpgan_train
@@ -76,29 +83,47 @@ def main():
     torch.manual_seed(1234)
     G = DG.Generator(GCFG["zdim"], GCFG["num_classes"], use_batchnorm=False).to(dev)
     D = DG.Discriminator().to(dev)
-    tr = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16)
+    idf = None
+    if a.identity != "none":
+        import FeatureExtract as FE
+        idf = FE.IdentityPreservingLoss(FE.FeatureExtractModel(a.identity, 347).to(dev), torch.bfloat16)
+    tr = tpgan_train.TPGANTrainer(G, D, lr=1e-4, compute_dtype=torch.bfloat16, identity_fn=idf, gradient_penalty=a.gp)
     TRAINER[0] = tr
     b = tpgan_train.synthetic_batch(a.batch, dev, seed=1000)
     variants = [parse_variant(v) for v in a.variants]  # (after TRAINER is set)
-    for name, sets in variants:  # warm-up under every variant (autotuning, first-use packing)
+    streams = {}
+
+    def run_steps(prio, n):
+        if prio is None:
+            for _ in range(n):
+                tr.step(b, next_b=b)
+            return
+        st = streams.get(prio)
+        if st is None:
+            st = streams[prio] = torch.cuda.Stream(priority=prio)
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            for _ in range(n):
+                tr.step(b, next_b=b)
+        torch.cuda.current_stream().wait_stream(st)
+
+    for name, sets, prio in variants:  # warm-up under every variant (autotuning, first-use packing)
         old = apply(sets)
-        for _ in range(a.warmup):
-            tr.step(b, next_b=b)
+        run_steps(prio, a.warmup)
         restore(old)
     torch.cuda.synchronize()
-    res = {name: [] for name, _ in variants}
+    res = {name: [] for name, _, _ in variants}
     for r in range(a.rounds):
-        for name, sets in variants:
+        for name, sets, prio in variants:
             old = apply(sets)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(a.steps):
-                tr.step(b, next_b=b)
+            run_steps(prio, a.steps)
             torch.cuda.synchronize()
             res[name].append((time.perf_counter() - t0) / a.steps * 1e3)
             restore(old)
-        print("round %d: %s" % (r, "  ".join("%s %.3f" % (n, res[n][-1]) for n, _ in variants)), flush=True)
-    for name, _ in variants:
+        print("round %d: %s" % (r, "  ".join("%s %.3f" % (n, res[n][-1]) for n, _, _ in variants)), flush=True)
+    for name, _, _ in variants:
         v = res[name]
         print("%-12s median %.3f ms/step  min %.3f  (%s)" % (name, statistics.median(v), min(v),
                                                           " ".join("%.2f" % x for x in v)))
