@@ -96,6 +96,9 @@ typedef struct tpg_conv_desc {
                                      once per b-tile); -30 when not covered */
   int32_t flags;                  /* TPG_FLAG_*: WPACKED = w.data is the image tpg_conv2d_pack_jobs /
                                      tpg_pack_run produced for this descriptor and op */
+  int32_t data_ksplit;            /* 0 = automatic; >= 1 forces the k-step split of the forward and
+                                     input-gradient launches (1: no split, so no split-K finish
+                                     launch); set by autotuners; ignored in deterministic mode */
 } tpg_conv_desc;
 
 enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2, TPG_FLAG_DX_ACCUM = 4 };

@@ -155,6 +155,7 @@ int main(int argc, char** argv) {
     d.pad_mode = (!d.transposed && rnd() % 5 == 0) ? TPG_PAD_REFLECT : TPG_PAD_ZERO;
     d.act = rnd() % 4; d.slope = 0.2f; d.res_scale = 1.f;
     d.ksplit = rnd() % 3 ? 0 : 1 + rnd() % 16;
+    d.data_ksplit = rnd() % 3 ? 0 : 1 + rnd() % 64;
     d.algo = rnd() % 3 ? 0 : (int)(rnd() % 14) - 1;
     d.flags = rnd() % 8;
     if (d.transposed) {

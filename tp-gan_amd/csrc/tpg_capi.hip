@@ -49,13 +49,16 @@ static int g_det = 0;  // tpg_set_deterministic
 // (the op runs beside other streams' work, e.g. the four local pathways: fewer K / pixel
 // splits, since the other streams fill the CUs a split would).  Set per entry point.
 static thread_local int g_share = 1;
+// forced k-step split of the forward / input-gradient launches (desc.data_ksplit; 0 = planner)
+static thread_local int g_data_ks = 0;
 struct ShareScope {
-  int prev;
-  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share) {
+  int prev, prev_ks;
+  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share), prev_ks(g_data_ks) {
+    g_data_ks = (d && d->data_ksplit > 0) ? d->data_ksplit : 0;
     // (1/2 .. 1/8 measured within run-to-run spread, profiles/r02c/share)
     g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? 4 : 1;
   }
-  ~ShareScope() { g_share = prev; }
+  ~ShareScope() { g_share = prev; g_data_ks = prev_ks; }
 };
 
 int tpg::deterministic() { return __atomic_load_n(&g_det, __ATOMIC_RELAXED); }
@@ -299,8 +302,9 @@ static void finish(Prob& P, int dtype, int M) {
   const int blocks = cdiv(M, bm) * (npad / bn);
   a.ksplit = 1;
   a.kt_per_split = std::max(nkt, 1);
-  if (blocks < 480 / g_share && nkt >= 8 && !deterministic()) {
-    int ks = std::min(cdiv(960 / g_share, blocks), nkt / 4);
+  if (!deterministic() && (g_data_ks > 0 || (blocks < 480 / g_share && nkt >= 8))) {
+    int ks = g_data_ks > 0 ? std::min(g_data_ks, std::max(nkt, 1))  // (an autotuner's pick)
+                           : std::min(cdiv(960 / g_share, blocks), nkt / 4);
     if (ks > 1) {
       a.kt_per_split = cdiv(nkt, ks);
       a.ksplit = cdiv(nkt, a.kt_per_split);
@@ -552,6 +556,7 @@ static void maybe_halo(Prob& P, int dtype, int N) {
     const int kps_min = cdiv(split_steps, a.ntaps);
     ks = (int)std::min<int64_t>(cdiv(split_to / g_share, (int)base), std::max(1, h.nks / kps_min));
   }
+  if (g_data_ks > 0 && !deterministic()) ks = std::min(g_data_ks, h.nks);  // (an autotuner's pick)
   h.kps = cdiv(h.nks, std::max(ks, 1));
   h.ksplit = cdiv(h.nks, h.kps);
   P.halo = true;

@@ -367,6 +367,80 @@ def _time_wgrad(lib, d, x, g, scratch):
     return [t]
 
 
+# Forward / input-gradient k-split autotuning (desc.data_ksplit): the planner splits the k-steps
+# of a small grid (< 256 blocks) over more blocks and finishes with a split-K epilogue launch; on
+# the small maps a shape's best split -- or none, which drops the epilogue launch -- is timed on
+# first use like the weight gradient's tile (graph replays of the candidate launches).
+# Measured on configs[1] (profiles/r04/data_split_tuner.txt): 8 of 90 shapes re-picked, ~0.1 ms
+# of isolated wins, the step unchanged (33.33 vs 33.33 ms interleaved) -- off by default.
+_DATA_SPLITS = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
+DATA_TUNE = {"enabled": False, "log": None}  # log: a list to append (op, shape, {split: ms}, pick) to
+_DATA_SPLIT_WS_CAP = 256 << 20
+
+
+def _time_launches(fn, reps=_TUNE_REPS):
+    """GPU ms per call of fn (a launch on the current stream), from a replayed HIP graph."""
+    gr = torch.cuda.CUDAGraph()
+    cs = _tune_stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        gr.capture_begin(capture_error_mode="thread_local")
+        try:
+            for _ in range(reps):
+                fn()
+        finally:
+            gr.capture_end()
+    gr.replay()  # (replays run on the current stream)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    gr.replay()
+    e1.record()
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / reps
+    del gr
+    return t
+
+
+def _tuned_data_split(lib, d, op, device, launch):
+    """data_ksplit for this (op, shape): on first use every candidate split is timed through
+    launch(ws) with d.data_ksplit set (a workspace sized for it); a split other than the
+    planner's own (0) must win by 10 %.  Returns the pick (also left in d.data_ksplit)."""
+    d.data_ksplit = 0
+    if not (AUTOTUNE["enabled"] and DATA_TUNE["enabled"]) or d.dtype == TPG_F32 or lib.tpg_get_deterministic():
+        return 0
+    key = ("dsplit", op, _desc_tuple(d) + (int(d.flags & FLAG_CONCURRENT), d.act))
+    hit = AUTOTUNE["cache"].get(key)
+    if hit is not None:
+        d.data_ksplit = hit[0]
+        return hit[0]
+    if torch.cuda.is_current_stream_capturing():
+        return 0
+    times = {}
+    torch.cuda.synchronize()
+    for ks in _DATA_SPLITS:
+        d.data_ksplit = ks
+        if ks > 1 and lib.tpg_conv2d_workspace(ctypes.byref(d), op) > _DATA_SPLIT_WS_CAP:
+            continue  # (a split this large never won; its partials would not fit L2 / MALL anyway)
+        ws = _ws(lib, d, op, device)
+        rc = launch(ws)
+        if rc:
+            continue
+        times[ks] = _time_launches(lambda: check(launch(ws)))
+        AUTOTUNE["trials"] += 1
+    best = 0
+    if times:
+        kbest = min(times, key=times.get)
+        if 0 not in times or times[kbest] < 0.9 * times[0]:
+            best = kbest
+    torch.cuda.synchronize()
+    AUTOTUNE["cache"][key] = (best, 0)
+    if DATA_TUNE["log"] is not None:
+        DATA_TUNE["log"].append((op, _desc_tuple(d)[:8], times, best))
+    d.data_ksplit = best
+    return best
+
+
 def _tuned_wgrad(lib, d, x, g, dwv):
     """(algo, ksplit) for this weight-gradient shape, tuning it on first use (pixel splits
     capped at 16 for ops planned for a share of the chip)."""
@@ -503,7 +577,7 @@ _WS_BYTES = {}  # (op, descriptor) -> workspace bytes: the C planner runs once p
 
 
 def _ws(lib, desc, op, device):
-    key = (op, desc.flags, desc.algo, desc.ksplit, lib.tpg_get_deterministic()) + _desc_tuple(desc)
+    key = (op, desc.flags, desc.algo, desc.ksplit, desc.data_ksplit, lib.tpg_get_deterministic()) + _desc_tuple(desc)
     nb = _WS_BYTES.get(key)
     if nb is None:
         nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
@@ -536,12 +610,24 @@ def _conv_act_forward(ctx, x, weight, bias, residual, geom, act, slope, res_scal
         if tuple(res.shape) != (n, cout, oh, ow):
             raise RuntimeError("residual shape %s != output %s" % (tuple(res.shape), (n, cout, oh, ow)))
     d = geom.desc(n, cin, h, w, cout, oh, ow, dtype, act, slope, res_scale)
-    ws = _ws(lib, d, OP_FWD, x.device)
     wv = weight if weight.dtype == torch.float32 else weight.float()
-    FLOPS["fwd"] += _conv_flops(d)
-    e0 = _probe_begin(d, "fwd")
     pk = _packed_weight(wparam if wparam is not None else weight, d, OP_FWD, wv)
     bptr = bias.data_ptr() if bias is not None else None
+    if keep is None:
+        def launch(ws_):
+            if pk is not None:
+                d.flags = d.flags | FLAG_WPACKED
+                try:
+                    return lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), _packed_tt(pk), bptr, tt(res), tt(_fix_c1(y)),
+                                              ws_.data_ptr(), ws_.numel(), stream_ptr())
+                finally:
+                    d.flags = d.flags & ~FLAG_WPACKED
+            return lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), bptr, tt(res), tt(_fix_c1(y)), ws_.data_ptr(),
+                                      ws_.numel(), stream_ptr())
+        _tuned_data_split(lib, d, OP_FWD, x.device, launch)
+    ws = _ws(lib, d, OP_FWD, x.device)
+    FLOPS["fwd"] += _conv_flops(d)
+    e0 = _probe_begin(d, "fwd")
     _run_maybe_packed(
         lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), _packed_tt(pk), bptr, tt(res), tt(_fix_c1(y)),
                                    ws.data_ptr(), ws.numel(), stream_ptr()),
@@ -585,6 +671,7 @@ class _ConvAct(torch.autograd.Function):
         lib = load()
         x, weight, y = ctx.saved_tensors
         d = ctx.d
+        d.data_ksplit = 0  # (the forward's pick)
         dtype = y.dtype
         n, cout, oh, ow = y.shape
         g = new_act(n, cout, oh, ow, dtype, y.device)
@@ -698,6 +785,27 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
                 dw = dw.contiguous(memory_format=torch.channels_last)
             dwv = dw
     wv = weight if weight.dtype == torch.float32 else weight.float()
+    d.data_ksplit = 0  # (ctx.d carries the forward's pick)
+    pk = _packed_weight(ctx.wparam, d, OP_BWD_DATA, wv) if need_dx else None
+    if need_dx and not grouped:
+        # the input-gradient launch's k split, tuned on first use into scratch g / dx (the real
+        # dx may hold a parked shortcut gradient it accumulates into)
+        sc = []
+
+        def launch(ws_):
+            if not sc:
+                sc.extend([_fix_c1(new_act(n, cout, oh, ow, dtype, y.device)), _fix_c1(new_act(*x.shape, dtype=dtype,
+                                                                                               device=x.device))])
+            if pk is not None:
+                d.flags = d.flags | FLAG_WPACKED
+            try:
+                return lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk) if pk is not None else tt(wv), tt(y),
+                                          tt(gy), tt(gy if g_is_gy else sc[0]), tt(sc[1]), tt(None), None,
+                                          ws_.data_ptr(), ws_.numel(), stream_ptr())
+            finally:
+                d.flags = d.flags & ~FLAG_WPACKED
+        _tuned_data_split(lib, d, OP_BWD_DATA, x.device, launch)
+        del sc
     ws = _ws(lib, d, OP_BWD_DATA, x.device) if need_dx else None
     wsp, wsn = (ws.data_ptr(), ws.numel()) if ws is not None else (None, 0)
     # the weight-gradient tile / split is autotuned on a shape's first call, which needs g:
@@ -711,7 +819,6 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
         FLOPS["dgrad"] += _conv_flops(d)
     if need_dw:
         FLOPS["wgrad"] += _conv_flops(d)
-    pk = _packed_weight(ctx.wparam, d, OP_BWD_DATA, wv) if need_dx else None
     fx = _fix_c1(dx) if dx is not None else None
     dwt = dwv if (need_dw and not tune_first) else None
     bptr = dbias.data_ptr() if dbias is not None else None
@@ -820,7 +927,7 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
 def _plain_desc(d):
     e = ConvDesc()
     ctypes.memmove(ctypes.byref(e), ctypes.byref(d), ctypes.sizeof(ConvDesc))
-    e.act, e.slope, e.res_scale, e.ksplit, e.algo = ACT_NONE, 0.0, 1.0, 0, 0
+    e.act, e.slope, e.res_scale, e.ksplit, e.algo, e.data_ksplit = ACT_NONE, 0.0, 1.0, 0, 0, 0
     return e
 
 
