@@ -58,6 +58,33 @@ SHAPES = {
     "local_img": (32, 64, 40, 40, 3, 1, 1, 0, False, 0, ACT_NONE, False),
     "local_fold": (32, 27, 40, 40, 64, 1, 1, 0, False, 0, ACT_LEAKY, False),
 }
+# ResNet-50 identity extractor (configs[2], ResNet.py Bottleneck; BN folded: bias + ReLU) on the
+# 128 x 128 G output, bs32: one line per distinct shape, with its count per forward pass
+R50 = {
+    "r50_conv1": ((32, 3, 128, 128, 64, 7, 2, 3, False, 0, ACT_RELU, False), 1),
+    "r50_l1_a0": ((32, 64, 32, 32, 64, 1, 1, 0, False, 0, ACT_RELU, False), 1),
+    "r50_l1_a": ((32, 256, 32, 32, 64, 1, 1, 0, False, 0, ACT_RELU, False), 2),
+    "r50_l1_b": ((32, 64, 32, 32, 64, 3, 1, 1, False, 0, ACT_RELU, False), 3),
+    "r50_l1_c": ((32, 64, 32, 32, 256, 1, 1, 0, False, 0, ACT_RELU, True), 4),
+    "r50_l2_a0": ((32, 256, 32, 32, 128, 1, 1, 0, False, 0, ACT_RELU, False), 1),
+    "r50_l2_b0": ((32, 128, 32, 32, 128, 3, 2, 1, False, 0, ACT_RELU, False), 1),
+    "r50_l2_ds": ((32, 256, 32, 32, 512, 1, 2, 0, False, 0, ACT_NONE, False), 1),
+    "r50_l2_a": ((32, 512, 16, 16, 128, 1, 1, 0, False, 0, ACT_RELU, False), 3),
+    "r50_l2_b": ((32, 128, 16, 16, 128, 3, 1, 1, False, 0, ACT_RELU, False), 3),
+    "r50_l2_c": ((32, 128, 16, 16, 512, 1, 1, 0, False, 0, ACT_RELU, True), 4),
+    "r50_l3_a0": ((32, 512, 16, 16, 256, 1, 1, 0, False, 0, ACT_RELU, False), 1),
+    "r50_l3_b0": ((32, 256, 16, 16, 256, 3, 2, 1, False, 0, ACT_RELU, False), 1),
+    "r50_l3_ds": ((32, 512, 16, 16, 1024, 1, 2, 0, False, 0, ACT_NONE, False), 1),
+    "r50_l3_a": ((32, 1024, 8, 8, 256, 1, 1, 0, False, 0, ACT_RELU, False), 5),
+    "r50_l3_b": ((32, 256, 8, 8, 256, 3, 1, 1, False, 0, ACT_RELU, False), 5),
+    "r50_l3_c": ((32, 256, 8, 8, 1024, 1, 1, 0, False, 0, ACT_RELU, True), 6),
+    "r50_l4_a0": ((32, 1024, 8, 8, 512, 1, 1, 0, False, 0, ACT_RELU, False), 1),
+    "r50_l4_b0": ((32, 512, 8, 8, 512, 3, 2, 1, False, 0, ACT_RELU, False), 1),
+    "r50_l4_ds": ((32, 1024, 8, 8, 2048, 1, 2, 0, False, 0, ACT_NONE, False), 1),
+    "r50_l4_a": ((32, 2048, 4, 4, 512, 1, 1, 0, False, 0, ACT_RELU, False), 2),
+    "r50_l4_b": ((32, 512, 4, 4, 512, 3, 1, 1, False, 0, ACT_RELU, False), 2),
+    "r50_l4_c": ((32, 512, 4, 4, 2048, 1, 1, 0, False, 0, ACT_RELU, True), 3),
+}
 
 
 def flops(s):
@@ -95,7 +122,7 @@ def timed(fn, iters, graph):
     return e0.elapsed_time(e1) / iters
 
 
-def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False):
+def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=()):
     lib = load()
     dev = torch.device("cuda", 0)
     N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
@@ -159,6 +186,23 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False):
         ms = timed(fn, iters, graph)
         tf = f / (ms * 1e-3) / 1e12
         out.append("%s %.3f ms %.0f TF/s (%.1f%%)" % (kind, ms, tf, 100 * tf / 2500))
+        if dsplits and kind in ("fwd", "dgrad"):  # forced forward / input-gradient k splits (desc.data_ksplit)
+            op = OP_FWD if kind == "fwd" else OP_BWD_DATA
+            alt = []
+            for ks in dsplits:
+                d.data_ksplit = ks
+                nb = lib.tpg_conv2d_workspace(ctypes.byref(d), op)
+                wsk = torch.empty(nb, dtype=torch.uint8, device=dev)
+                if kind == "fwd":
+                    fk = lambda: check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w), b.data_ptr() if act else None,
+                                                          tt(res), tt(y), wsk.data_ptr(), wsk.numel(), stream_ptr()))
+                else:
+                    fk = lambda: check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w), tt(dx), wsk.data_ptr(),
+                                                               wsk.numel(), stream_ptr()))
+                fk()
+                alt.append("%d:%.3f" % (ks, timed(fk, iters, graph)))
+            d.data_ksplit = 0
+            out.append("splits " + " ".join(alt))
     print("%-12s %6.1f GF | %s" % (name, f / 1e9, " | ".join(out)), flush=True)
 
 
@@ -171,18 +215,22 @@ def main():
     ap.add_argument("--wg-algo", default="",
                     help="weight-gradient algo[/pixel splits] per shape, e.g. enhance_128=12/1,add_128=7")
     ap.add_argument("--graph", action="store_true", help="time graph replays (GPU time of short kernels)")
+    ap.add_argument("--r50", action="store_true", help="the ResNet-50 identity extractor's shapes (configs[2])")
+    ap.add_argument("--dsplits", default="", help="also time forced fwd / dgrad k splits, e.g. 1,2,4,8")
     ap.add_argument("--tune-file", default=None,
                     help="weight-gradient picks saved by a train step (bench.py with TPG_TUNE_DUMP=path)")
     a = ap.parse_args()
     if a.tune_file:
         T.load_tuning(a.tune_file)
-    for name, s in SHAPES.items():
+    shapes = {k: v[0] for k, v in R50.items()} if a.r50 else SHAPES
+    ds = tuple(int(v) for v in a.dsplits.split(",") if v)
+    for name, s in shapes.items():
         if a.only and name not in a.only.split(","):
             continue
         algos = dict(kv.split("=") for kv in a.wg_algo.split(",") if kv)
         al = algos.get(name, "0").split("/")
         run(name, s, a.iters, a.passes.split(","), a.wg_sweep, (int(al[0]), int(al[1]) if len(al) > 1 else 0),
-            a.graph)
+            a.graph, ds)
 
 
 if __name__ == "__main__":

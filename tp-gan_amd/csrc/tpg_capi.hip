@@ -197,6 +197,10 @@ static GLaunch& grec(int kind, hipStream_t s, int dtype) {
 }
 
 static int do_halo(const HaloArgs& h, int dtype, int cfg, hipStream_t s, bool mask) {
+  if (h.pw > 0 && !mask) {  // (not a launch-group kernel: the recorded launches go first)
+    const int rc = group_flush();
+    return rc ? rc : launch_pw(h, dtype, s);
+  }
   if (!g_grp.active) return launch_halo(h, dtype, cfg, s, mask);
   GLaunch& L = grec(1, s, dtype);
   L.h = h; L.cfg = cfg; L.mask = mask;
@@ -557,6 +561,24 @@ static void maybe_halo(Prob& P, int dtype, int N) {
     ks = (int)std::min<int64_t>(cdiv(split_to / g_share, (int)base), std::max(1, h.nks / kps_min));
   }
   if (g_data_ks > 0 && !deterministic()) ks = std::min(g_data_ks, h.nks);  // (an autotuner's pick)
+  // one tap (1x1 convs, stride 1 or 2) on whole 32-channel k-steps: the pointwise GEMM kernel,
+  // whose 4-stage DMA ring hides the loads this kernel exposes every k-step when there is only
+  // one tap per step; the largest of its tiles that still gives a chip's worth of blocks, and a
+  // k split only for the few-block problems
+  h.pw = 0;
+  if (a.ntaps == 1 && a.dil <= 1 && half16(dtype) && a.C % 32 == 0 && (bn == 64 || bn == 128)) {
+    const int64_t M = (int64_t)N * JH * JW;
+    int64_t bb = 0;
+    for (int c = 1; c <= 4; ++c) {
+      if (pw_tile_bn(c) > bn) continue;
+      const int64_t blocks = cdiv(M, pw_tile_bm(c)) * (int64_t)cdiv(a.Nout, pw_tile_bn(c));
+      if (blocks > bb) { h.pw = c; bb = blocks; }
+      if (blocks >= 240 / g_share) { h.pw = c; bb = blocks; break; }
+    }
+    ks = 1;
+    if (bb < 128 / g_share && !deterministic()) ks = (int)std::min<int64_t>(cdiv(256 / g_share, (int)bb), h.nks / 8);
+    if (g_data_ks > 0 && !deterministic()) ks = std::min(g_data_ks, h.nks);
+  }
   h.kps = cdiv(h.nks, std::max(ks, 1));
   h.ksplit = cdiv(h.nks, h.kps);
   P.halo = true;

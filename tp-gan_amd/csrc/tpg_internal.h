@@ -362,6 +362,7 @@ struct HaloArgs {
   int ntaps;
   int dymin, dxmin, HH, HW;   // halo of one sub-tile = HH x HW pixels
   int pad_mode, vec_ok;        // vec_ok: 16-byte loads of whole chunks stay inside each pixel row
+  int pw;                     // > 0: one-tap problem on the pointwise GEMM kernel, tile config (tpg_pw.hip)
   int N, JH, JW, tiles_h, tiles_w;
   int TH, TW, IMG, SH, SW;    // sub-tile shape, sub-tiles per block, A-grid stride of the taps
   int dil;                    // > 1: halo coordinates are on A dilated by dil (zero between real pixels)
@@ -466,6 +467,11 @@ int halo_cfg(int hl, int bn);
 size_t halo_lds_bytes(int hcap, int bn, int rs = 3, int bm = 256);
 int halo_cfg512(int bn);
 int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask = false);
+// pointwise (1x1) GEMM kernel on a one-tap halo plan (a.pw = tile config 1..4: 128x128, 128x64,
+// 64x128, 64x64 rows x output channels); same packed weights, epilogue and split-K slices
+int launch_pw(const HaloArgs& a, int dtype, hipStream_t s);
+int pw_tile_bm(int cfg);
+int pw_tile_bn(int cfg);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
 size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
 

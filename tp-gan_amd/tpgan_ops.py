@@ -371,10 +371,10 @@ def _time_wgrad(lib, d, x, g, scratch):
 # of a small grid (< 256 blocks) over more blocks and finishes with a split-K epilogue launch; on
 # the small maps a shape's best split -- or none, which drops the epilogue launch -- is timed on
 # first use like the weight gradient's tile (graph replays of the candidate launches).
-# Measured on configs[1] (profiles/r04/data_split_tuner.txt): 8 of 90 shapes re-picked, ~0.1 ms
-# of isolated wins, the step unchanged (33.33 vs 33.33 ms interleaved) -- off by default.
+# Measured (profiles/r04/data_split_tuner.txt): configs[1] re-picks 8 of 90 shapes, step unchanged
+# (33.33 vs 33.33 ms interleaved); configs[2]'s ResNet-50 layers gain 38.36 -> 37.93 ms/step.
 _DATA_SPLITS = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
-DATA_TUNE = {"enabled": False, "log": None}  # log: a list to append (op, shape, {split: ms}, pick) to
+DATA_TUNE = {"enabled": True, "log": None}  # log: a list to append (op, shape, {split: ms}, pick) to
 _DATA_SPLIT_WS_CAP = 256 << 20
 
 
