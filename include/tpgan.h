@@ -99,6 +99,10 @@ typedef struct tpg_conv_desc {
   int32_t data_ksplit;            /* 0 = automatic; >= 1 forces the k-step split of the forward and
                                      input-gradient launches (1: no split, so no split-K finish
                                      launch); set by autotuners; ignored in deterministic mode */
+  int32_t data_algo;              /* forward / input-gradient kernel of small-map convs with several
+                                     taps: 0 = planner's rule, 1 = the halo-tiled kernel, 2 = the
+                                     tap-DMA pointwise kernel where eligible (16-bit, channels a
+                                     multiple of 32); set by autotuners */
 } tpg_conv_desc;
 
 enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2, TPG_FLAG_DX_ACCUM = 4 };

@@ -33,11 +33,11 @@ def main():
     torch.cuda.synchronize()
     names = {0: "fwd", 1: "dgrad"}
     print("op     n  cin  h    w  cout oh   ow   pick  t(0) ms   t(pick) ms  candidates")
-    for op, shp, times, best in sorted(log, key=lambda e: -(e[2].get(0, 0.0))):
-        t0 = times.get(0, float("nan"))
+    for op, shp, times, best in sorted(log, key=lambda e: -(e[2].get((0, 0), 0.0))):
+        t0 = times.get((0, 0), float("nan"))
         tb = times.get(best, float("nan"))
-        cand = " ".join("%d:%.4f" % (k, v) for k, v in sorted(times.items()))
-        print("%-5s %s  %3d  %.4f  %.4f  %s" % (names.get(op, op), " ".join("%4d" % v for v in shp[:7]), best, t0,
+        cand = " ".join("%s/%s:%.4f" % (k[1], k[0], v) for k, v in sorted(times.items()))
+        print("%-5s %s  %s  %.4f  %.4f  %s" % (names.get(op, op), " ".join("%4d" % v for v in shp[:7]), best, t0,
                                                  tb, cand))
     for en in (True, False):
         tpgan_ops.DATA_TUNE["enabled"] = en

@@ -156,6 +156,7 @@ int main(int argc, char** argv) {
     d.act = rnd() % 4; d.slope = 0.2f; d.res_scale = 1.f;
     d.ksplit = rnd() % 3 ? 0 : 1 + rnd() % 16;
     d.data_ksplit = rnd() % 3 ? 0 : 1 + rnd() % 64;
+    d.data_algo = rnd() % 3 ? 0 : (int)(rnd() % 4) - 1;
     d.algo = rnd() % 3 ? 0 : (int)(rnd() % 14) - 1;
     d.flags = rnd() % 8;
     if (d.transposed) {

@@ -49,16 +49,23 @@ static int g_det = 0;  // tpg_set_deterministic
 // (the op runs beside other streams' work, e.g. the four local pathways: fewer K / pixel
 // splits, since the other streams fill the CUs a split would).  Set per entry point.
 static thread_local int g_share = 1;
+// small-map convs with several taps on the pointwise kernel (tpg_pw.hip; 0: the halo kernel, A/B)
+#ifndef TPG_PW_TAPS
+#define TPG_PW_TAPS 1
+#endif
 // forced k-step split of the forward / input-gradient launches (desc.data_ksplit; 0 = planner)
 static thread_local int g_data_ks = 0;
+// kernel of the small-map multi-tap forward / input-gradient plans (desc.data_algo; 0 = rule)
+static thread_local int g_data_algo = 0;
 struct ShareScope {
-  int prev, prev_ks;
-  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share), prev_ks(g_data_ks) {
+  int prev, prev_ks, prev_algo;
+  explicit ShareScope(const tpg_conv_desc* d) : prev(g_share), prev_ks(g_data_ks), prev_algo(g_data_algo) {
     g_data_ks = (d && d->data_ksplit > 0) ? d->data_ksplit : 0;
+    g_data_algo = (d && (d->data_algo == 1 || d->data_algo == 2)) ? d->data_algo : 0;
     // (1/2 .. 1/8 measured within run-to-run spread, profiles/r02c/share)
     g_share = (d && (d->flags & TPG_FLAG_CONCURRENT)) ? 4 : 1;
   }
-  ~ShareScope() { g_share = prev; g_data_ks = prev_ks; }
+  ~ShareScope() { g_share = prev; g_data_ks = prev_ks; g_data_algo = prev_algo; }
 };
 
 int tpg::deterministic() { return __atomic_load_n(&g_det, __ATOMIC_RELAXED); }
@@ -565,12 +572,18 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   // whose 4-stage DMA ring hides the loads this kernel exposes every k-step when there is only
   // one tap per step; the largest of its tiles that still gives a chip's worth of blocks, and a
   // k split only for the few-block problems
+  // Several taps: the same kernel (tap-shifted A rows by DMA, no reuse of a halo across taps)
+  // where the halo grid is too small for the chip and would split K and the input is at most 256
+  // channels deep (measured: local_20 128 ch 0.034 -> 0.021 ms, ResNet-50 l2 3x3 0.028 -> 0.018;
+  // 512 / 768-channel maps slower, they keep the halo); desc.data_algo overrides (autotuner)
+  const bool small_map = a.ntaps > 1 && (g_data_algo == 2 || (g_data_algo == 0 && TPG_PW_TAPS &&
+                                                              base < split_below / g_share && a.C <= 256));
   h.pw = 0;
-  if (a.ntaps == 1 && a.dil <= 1 && half16(dtype) && a.C % 32 == 0 && (bn == 64 || bn == 128)) {
+  if ((a.ntaps == 1 || small_map) && a.dil <= 1 && half16(dtype) && a.C % 32 == 0 && bn % 64 == 0 && bn <= 192) {
     const int64_t M = (int64_t)N * JH * JW;
     int64_t bb = 0;
     for (int c = 1; c <= 4; ++c) {
-      if (pw_tile_bn(c) > bn) continue;
+      if (pw_tile_bn(c) > bn || bn % pw_tile_bn(c)) continue;
       const int64_t blocks = cdiv(M, pw_tile_bm(c)) * (int64_t)cdiv(a.Nout, pw_tile_bn(c));
       if (blocks > bb) { h.pw = c; bb = blocks; }
       if (blocks >= 240 / g_share) { h.pw = c; bb = blocks; break; }

@@ -30,10 +30,12 @@ __device__ __forceinline__ int pw_swz(int row) { return ((row >> 2) & 1) << 1; }
 __device__ u32x4 pw_zero[4];  // the zero line of out-of-grid A rows (64 bytes)
 
 __host__ __device__ constexpr int pw_stage_bytes(int bm, int bn) { return (bm + bn) * 64; }
+// the ring (or the epilogue's parked rows, whichever is larger), then the tap table
 __host__ __device__ constexpr int pw_lds_bytes(int bm, int bn) {
-  return (PW_NST * pw_stage_bytes(bm, bn) > bm * 16 + 512 * 4 + bm * (bn + 4) * 4)
-             ? PW_NST * pw_stage_bytes(bm, bn)
-             : bm * 16 + 512 * 4 + bm * (bn + 4) * 4;
+  return ((PW_NST * pw_stage_bytes(bm, bn) > bm * 16 + 512 * 4 + bm * (bn + 4) * 4)
+              ? PW_NST * pw_stage_bytes(bm, bn)
+              : bm * 16 + 512 * 4 + bm * (bn + 4) * 4) +
+         TPG_MAX_TAPS * 4;
 }
 
 template <int N_>
@@ -75,46 +77,62 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
 
   // ---- A: this thread's DMA chunks (piece j of wave w covers 16-byte slots (j*4 + w)*64 + lane
   // of the A image, slot s = row * 4 + physical chunk; the source is the row's logical chunk
-  // (s & 3) ^ swz(row)); rows outside the grid / image read a zero line that does not advance
-  // (LDS-DMA through inline asm, as the halo kernel's weights: the builtin would make the
-  // compiler wait for every DMA in flight before each fragment read)
-  const char* asrc[PA];
-  int ainc[PA];
+  // (s & 3) ^ swz(row)) of the row's pixel shifted by the step's tap; rows outside the grid and
+  // taps outside the image read a zero line (LDS-DMA through inline asm, as the halo kernel's
+  // weights: the builtin would make the compiler wait for every DMA in flight before each
+  // fragment read)
+  const int ntaps = p.ntaps, total = nks * ntaps;  // pipeline steps (k-step, tap), tap fastest
+  int* s_tap = reinterpret_cast<int*>(lds + pw_lds_bytes(BM, BN) - TPG_MAX_TAPS * 4);
+  if (tid < ntaps) {  // (dy - dymin) << 16 | (dx - dxmin) of each tap, from the halo shift table
+    const int dyr = p.toff[tid] / p.HW;
+    s_tap[tid] = (dyr << 16) | (p.toff[tid] - dyr * p.HW);
+  }
+  const char* abase[PA];
+  int agy[PA], agx[PA];
   const int JHW = p.JH * p.JW;
   const char* Ab = reinterpret_cast<const char*>(p.A);
+  const char* zline = reinterpret_cast<const char*>(pw_zero);
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int s = (j * 4 + wave) * 64 + lane;
     const int row = s >> 2, c = (s & 3) ^ pw_swz(row);
     const int q = m0 + row;
-    asrc[j] = reinterpret_cast<const char*>(pw_zero);
-    ainc[j] = 0;
+    abase[j] = nullptr;
+    agy[j] = agx[j] = 0;
     if (q < M) {
       const int nimg = q / JHW, r = q - nimg * JHW;
       const int jy = r / p.JW, ix = r - jy * p.JW;
-      const int gy = jy * p.SH + p.dymin, gx = ix * p.SW + p.dxmin;
-      if ((unsigned)gy < (unsigned)p.A_H && (unsigned)gx < (unsigned)p.A_W) {
-        asrc[j] = Ab + ((int64_t)nimg * p.a_sn + (int64_t)gy * p.a_sh + (int64_t)gx * p.a_sw + ks0 * KS + c * 8) *
-                           (int64_t)sizeof(E);
-        ainc[j] = KS * (int)sizeof(E);
-      }
+      agy[j] = jy * p.SH + p.dymin;
+      agx[j] = ix * p.SW + p.dxmin;
+      abase[j] = Ab + ((int64_t)nimg * p.a_sn + ks0 * KS + c * 8) * (int64_t)sizeof(E);
     }
   }
   // ---- B: the packed image [nks][ntiles][BNL][64 B] of the planner's BN (p.BN >= BN): this
   // tile's BN rows are contiguous
   const int BNLp = (p.BN + 127) / 128 * 128;
   const char* wsrc = reinterpret_cast<const char*>(p.Wp) +
-                     (((int64_t)ks0 * p.ntiles + n0 / p.BN) * BNLp + (n0 % p.BN)) * 64 + (wave * 1024 + lane * 16);
+                     (((int64_t)ks0 * ntaps * p.ntiles + n0 / p.BN) * BNLp + (n0 % p.BN)) * 64 + (wave * 1024 + lane * 16);
   const int64_t wstep = (int64_t)p.ntiles * BNLp * 64;
   // (M0 takes a wave-uniform LDS address: the wave index as a scalar)
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds)) +
                         (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 1024;
 
-  auto issue = [&](int ks, int st) {  // ks clamped by the caller
+  const int A_H = p.A_H, A_W = p.A_W, pad_mode = p.pad_mode;
+  const int64_t ash = p.a_sh * (int64_t)sizeof(E), asw = p.a_sw * (int64_t)sizeof(E);
+  auto issue = [&](int ks, int t, int st) {  // step (ks, t), clamped by the caller
     const uint32_t base = lds0 + (uint32_t)st * STAGE;
+    const int tap = s_tap[t];
 #pragma unroll
-    for (int j = 0; j < PA; ++j) lds_dma16(asrc[j] + ks * ainc[j], base + j * 4096);
-    const char* src = wsrc + (int64_t)ks * wstep;
+    for (int j = 0; j < PA; ++j) {
+      int y = agy[j] + (tap >> 16), x = agx[j] + (tap & 0xffff);
+      if (pad_mode) {  // (reflect: the mirrored pixel)
+        y = y < 0 ? -y : (y >= A_H ? 2 * A_H - 2 - y : y);
+        x = x < 0 ? -x : (x >= A_W ? 2 * A_W - 2 - x : x);
+      }
+      const bool ok = abase[j] != nullptr && (unsigned)y < (unsigned)A_H && (unsigned)x < (unsigned)A_W;
+      lds_dma16(ok ? abase[j] + y * ash + x * asw + ks * (KS * (int)sizeof(E)) : zline, base + j * 4096);
+    }
+    const char* src = wsrc + (int64_t)(ks * ntaps + t) * wstep;
 #pragma unroll
     for (int j = 0; j < PB; ++j) lds_dma16(src + j * 4096, base + BM * 64 + j * 4096);
   };
@@ -127,17 +145,29 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nks > 0) {
+  __syncthreads();  // (tap table)
+  if (total > 0) {
+    // issue cursor (iks, it): the step NST - 1 ahead of the one computed, held at the last step
+    int iks = 0, it = 0;
+    auto advance = [&]() {
+      if (iks * ntaps + it + 1 < total) {
+        if (++it == ntaps) { it = 0; ++iks; }
+      }
+    };
 #pragma unroll
-    for (int s = 0; s < NST - 1; ++s) issue(min(s, nks - 1), s);
+    for (int s = 0; s < NST - 1; ++s) {
+      issue(iks, it, s);
+      advance();
+    }
     int st = 0;
-    for (int ks = 0; ks < nks; ++ks) {
-      // k-step ks landed (the NST - 2 younger stages stay in flight); every wave is past
-      // k-step ks - 1, whose stage the next issue overwrites
+    for (int ks = 0; ks < total; ++ks) {
+      // step ks landed (the NST - 2 younger stages stay in flight); every wave is past step
+      // ks - 1, whose stage the next issue overwrites
       pw_wait_vm<(NST - 2) * (PA + PB)>();
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       const int sti = st == 0 ? NST - 1 : st - 1;  // (ks + NST - 1) % NST
-      issue(min(ks + NST - 1, nks - 1), sti);
+      issue(iks, it, sti);
+      advance();
       const char* A = lds + st * STAGE;
       const u32x4* B = reinterpret_cast<const u32x4*>(A + BM * 64);
       u32x4 af[MREP], bf[NREP];
@@ -272,9 +302,11 @@ static int launch_pw_t(const HaloArgs& a, hipStream_t s) {
 }
 
 int launch_pw(const HaloArgs& a, int dtype, hipStream_t s) {
-  // the kernel's assumptions (the planner only picks it when they hold): one tap, whole
+  // the kernel's assumptions (the planner only picks it when they hold): whole
   // 32-channel k-steps, a planner tile at least as wide as this one, 32-bit byte offsets
-  if (a.ntaps != 1 || a.dil > 1 || a.C % 32 || (dtype != 1 && dtype != 2) || a.pw < 1 || a.pw > 4) return -1;
+  if (a.ntaps < 1 || a.ntaps > TPG_MAX_TAPS || a.dil > 1 || a.C % 32 || (dtype != 1 && dtype != 2) || a.pw < 1 ||
+      a.pw > 4 || a.HW < 1 || a.HW >= (1 << 16))
+    return -1;
   const int bm = PW_BM[a.pw - 1], bn = PW_BN[a.pw - 1];
   if (a.BN < bn || a.BN % bn) return -1;
   const int64_t ext = ((int64_t)(a.N - 1) * a.a_sn + (int64_t)(a.A_H - 1) * a.a_sh + (int64_t)(a.A_W - 1) * a.a_sw + a.C) * 2;

@@ -33,7 +33,8 @@ class ConvDesc(ctypes.Structure):
         "n", "in_c", "in_h", "in_w", "out_c", "out_h", "out_w", "kh", "kw", "stride_h", "stride_w",
         "pad_t", "pad_b", "pad_l", "pad_r", "pad_mode", "transposed", "dtype", "act")] + [
         ("slope", ctypes.c_float), ("res_scale", ctypes.c_float), ("ksplit", ctypes.c_int32),
-        ("algo", ctypes.c_int32), ("flags", ctypes.c_int32), ("data_ksplit", ctypes.c_int32)]
+        ("algo", ctypes.c_int32), ("flags", ctypes.c_int32), ("data_ksplit", ctypes.c_int32),
+        ("data_algo", ctypes.c_int32)]
 
 
 FLAG_WPACKED = 1

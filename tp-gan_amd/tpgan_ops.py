@@ -373,7 +373,8 @@ def _time_wgrad(lib, d, x, g, scratch):
 # first use like the weight gradient's tile (graph replays of the candidate launches).
 # Measured (profiles/r04/data_split_tuner.txt): configs[1] re-picks 8 of 90 shapes, step unchanged
 # (33.33 vs 33.33 ms interleaved); configs[2]'s ResNet-50 layers gain 38.36 -> 37.93 ms/step.
-_DATA_SPLITS = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
+_DATA_SPLITS = (0, 1, 2, 4, 8, 16)
+_DATA_ALGOS = (1, 2)  # desc.data_algo: the halo-tiled kernel, the tap-DMA pointwise kernel
 DATA_TUNE = {"enabled": True, "log": None}  # log: a list to append (op, shape, {split: ms}, pick) to
 _DATA_SPLIT_WS_CAP = 256 << 20
 
@@ -403,41 +404,42 @@ def _time_launches(fn, reps=_TUNE_REPS):
 
 
 def _tuned_data_split(lib, d, op, device, launch):
-    """data_ksplit for this (op, shape): on first use every candidate split is timed through
-    launch(ws) with d.data_ksplit set (a workspace sized for it); a split other than the
-    planner's own (0) must win by 10 %.  Returns the pick (also left in d.data_ksplit)."""
-    d.data_ksplit = 0
+    """(data_ksplit, data_algo) for this (op, shape): on first use the planner's own plan and
+    every (kernel, split) candidate are timed through launch(ws) with the descriptor set (a
+    workspace sized for it); a candidate must beat the planner's plan by 10 %.  Returns the
+    pick (also left in d.data_ksplit / d.data_algo)."""
+    d.data_ksplit, d.data_algo = 0, 0
     if not (AUTOTUNE["enabled"] and DATA_TUNE["enabled"]) or d.dtype == TPG_F32 or lib.tpg_get_deterministic():
-        return 0
+        return (0, 0)
     key = ("dsplit", op, _desc_tuple(d) + (int(d.flags & FLAG_CONCURRENT), d.act))
     hit = AUTOTUNE["cache"].get(key)
     if hit is not None:
-        d.data_ksplit = hit[0]
-        return hit[0]
+        d.data_ksplit, d.data_algo = hit
+        return hit
     if torch.cuda.is_current_stream_capturing():
-        return 0
+        return (0, 0)
     times = {}
     torch.cuda.synchronize()
-    for ks in _DATA_SPLITS:
-        d.data_ksplit = ks
-        if ks > 1 and lib.tpg_conv2d_workspace(ctypes.byref(d), op) > _DATA_SPLIT_WS_CAP:
+    for cand in [(0, 0)] + [(ks, al) for al in _DATA_ALGOS for ks in _DATA_SPLITS]:
+        d.data_ksplit, d.data_algo = cand
+        if cand[0] > 1 and lib.tpg_conv2d_workspace(ctypes.byref(d), op) > _DATA_SPLIT_WS_CAP:
             continue  # (a split this large never won; its partials would not fit L2 / MALL anyway)
         ws = _ws(lib, d, op, device)
         rc = launch(ws)
         if rc:
             continue
-        times[ks] = _time_launches(lambda: check(launch(ws)))
+        times[cand] = _time_launches(lambda: check(launch(ws)))
         AUTOTUNE["trials"] += 1
-    best = 0
+    best = (0, 0)
     if times:
         kbest = min(times, key=times.get)
-        if 0 not in times or times[kbest] < 0.9 * times[0]:
+        if (0, 0) not in times or times[kbest] < 0.9 * times[(0, 0)]:
             best = kbest
     torch.cuda.synchronize()
-    AUTOTUNE["cache"][key] = (best, 0)
+    AUTOTUNE["cache"][key] = best
     if DATA_TUNE["log"] is not None:
         DATA_TUNE["log"].append((op, _desc_tuple(d)[:8], times, best))
-    d.data_ksplit = best
+    d.data_ksplit, d.data_algo = best
     return best
 
 
@@ -577,7 +579,8 @@ _WS_BYTES = {}  # (op, descriptor) -> workspace bytes: the C planner runs once p
 
 
 def _ws(lib, desc, op, device):
-    key = (op, desc.flags, desc.algo, desc.ksplit, desc.data_ksplit, lib.tpg_get_deterministic()) + _desc_tuple(desc)
+    key = ((op, desc.flags, desc.algo, desc.ksplit, desc.data_ksplit, desc.data_algo, lib.tpg_get_deterministic()) +
+           _desc_tuple(desc))
     nb = _WS_BYTES.get(key)
     if nb is None:
         nb = lib.tpg_conv2d_workspace(ctypes.byref(desc), op)
@@ -671,7 +674,7 @@ class _ConvAct(torch.autograd.Function):
         lib = load()
         x, weight, y = ctx.saved_tensors
         d = ctx.d
-        d.data_ksplit = 0  # (the forward's pick)
+        d.data_ksplit, d.data_algo = 0, 0  # (the forward's pick)
         dtype = y.dtype
         n, cout, oh, ow = y.shape
         g = new_act(n, cout, oh, ow, dtype, y.device)
@@ -785,7 +788,7 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
                 dw = dw.contiguous(memory_format=torch.channels_last)
             dwv = dw
     wv = weight if weight.dtype == torch.float32 else weight.float()
-    d.data_ksplit = 0  # (ctx.d carries the forward's pick)
+    d.data_ksplit, d.data_algo = 0, 0  # (ctx.d carries the forward's pick)
     pk = _packed_weight(ctx.wparam, d, OP_BWD_DATA, wv) if need_dx else None
     if need_dx and not grouped:
         # the input-gradient launch's k split, tuned on first use into scratch g / dx (the real
@@ -927,7 +930,7 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
 def _plain_desc(d):
     e = ConvDesc()
     ctypes.memmove(ctypes.byref(e), ctypes.byref(d), ctypes.sizeof(ConvDesc))
-    e.act, e.slope, e.res_scale, e.ksplit, e.algo, e.data_ksplit = ACT_NONE, 0.0, 1.0, 0, 0, 0
+    e.act, e.slope, e.res_scale, e.ksplit, e.algo, e.data_ksplit, e.data_algo = ACT_NONE, 0.0, 1.0, 0, 0, 0, 0
     return e
 
 
