@@ -225,6 +225,31 @@ int32_t tpg_grad_check(int64_t numel, const float* grad, float* state, tpg_strea
 
 /* ---- identity-feature extractors (MobileNetV2.py, ResNet.py, FeatureExtract.py) ---- */
 
+/* G-step image losses (tpgan_train._g_losses, build-defined; weights config.py:59-82) fused
+ * into single launches (SURVEY.md §3C loss suite).  x (the fake), r (the target), a_i, b_i:
+ * logical (n, c, h, w) views of any strides, TPG_F32 / TPG_BF16 / TPG_F16; gradients are
+ * written in the dtype and strides of the given tensor.  The forward writes one fp32 scalar
+ * to *out (device), summing fixed per-block partials in a fixed order (deterministic); ws:
+ * at least tpg_loss_workspace() bytes of device scratch.  Backward: gout = device pointer to
+ * the scalar's gradient.
+ *   image:  w_pix * mean|x - r| + w_sym * mean|x - flip_w(x)|
+ *           + w_tv * (mean|x[y+1] - x[y]| + mean|x[:, x+1] - x[:, x]|)
+ *   L1 set: sum_i weight_i * mean|a_i - b_i|   (da_i may have data NULL: no gradient) */
+#define TPG_L1_MAX_SEGS 8
+typedef struct tpg_l1_seg {
+  int32_t n, c, h, w;
+  tpg_tensor a, b, da;
+  float weight;
+} tpg_l1_seg;
+size_t tpg_loss_workspace(void);
+int32_t tpg_image_losses_fwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor x, tpg_tensor r, float w_pix,
+                             float w_sym, float w_tv, float* ws, size_t ws_bytes, float* out, tpg_stream_t stream);
+int32_t tpg_image_losses_bwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor x, tpg_tensor r, float w_pix,
+                             float w_sym, float w_tv, const float* gout, tpg_tensor dx, tpg_stream_t stream);
+int32_t tpg_l1_set_fwd(int32_t nseg, const tpg_l1_seg* segs, float* ws, size_t ws_bytes, float* out,
+                       tpg_stream_t stream);
+int32_t tpg_l1_set_bwd(int32_t nseg, const tpg_l1_seg* segs, const float* gout, tpg_stream_t stream);
+
 /* Depthwise Conv2d (groups == in_c == out_c, MobileNetV2.py:105), kernels up to 3x3, zero
  * padding: y = act(dwconv(x, w) + bias [+ res_scale * residual]).  w logical [C][1][kh][kw]
  * fp32 (any strides); x / y / residual channels-last, 16-byte aligned rows of desc.dtype. */

@@ -1340,6 +1340,70 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   return 0;
 }
 
+// ------------------------------------------------------------------ fused G losses --
+static constexpr size_t LOSS_WS = 512 * TPG_L1_MAX_SEGS * sizeof(float);  // (tpg_losses.hip LS_BLOCKS)
+extern "C" size_t tpg_loss_workspace(void) { return LOSS_WS; }
+
+static int32_t check_loss_tensor(const tpg_tensor& t, const char* what) {
+  if (!t.data) return fail(-10, "%s is NULL", what);
+  if (t.dtype != TPG_F32 && t.dtype != TPG_BF16 && t.dtype != TPG_F16) return fail(-11, "%s: bad dtype %d", what, t.dtype);
+  return 0;
+}
+
+extern "C" int32_t tpg_image_losses_fwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor x, tpg_tensor r,
+                                        float w_pix, float w_sym, float w_tv, float* ws, size_t ws_bytes, float* out,
+                                        tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc;
+  if (n < 1 || c < 1 || h < 1 || w < 1) return fail(-2, "image_losses: empty shape");
+  if ((rc = check_loss_tensor(x, "x")) || (rc = check_loss_tensor(r, "r"))) return rc;
+  if (!ws || ws_bytes < LOSS_WS || !out) return fail(-20, "image_losses: workspace / out");
+  return hip_check(launch_image_losses(n, c, h, w, x, r, w_pix, w_sym, w_tv, ws, nullptr, out, nullptr,
+                                       (hipStream_t)stream), "image_losses");
+}
+
+extern "C" int32_t tpg_image_losses_bwd(int32_t n, int32_t c, int32_t h, int32_t w, tpg_tensor x, tpg_tensor r,
+                                        float w_pix, float w_sym, float w_tv, const float* gout, tpg_tensor dx,
+                                        tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc;
+  if (n < 1 || c < 1 || h < 1 || w < 1) return fail(-2, "image_losses: empty shape");
+  if ((rc = check_loss_tensor(x, "x")) || (rc = check_loss_tensor(r, "r")) || (rc = check_loss_tensor(dx, "dx")))
+    return rc;
+  if (!gout) return fail(-10, "image_losses: gout is NULL");
+  return hip_check(launch_image_losses(n, c, h, w, x, r, w_pix, w_sym, w_tv, nullptr, gout, nullptr, &dx,
+                                       (hipStream_t)stream), "image_losses_bwd");
+}
+
+static int32_t check_l1_segs(int32_t nseg, const tpg_l1_seg* segs, bool bwd) {
+  if (nseg < 1 || nseg > TPG_L1_MAX_SEGS || !segs) return fail(-2, "l1_set: 1..%d segments", TPG_L1_MAX_SEGS);
+  for (int k = 0; k < nseg; ++k) {
+    const tpg_l1_seg& s = segs[k];
+    int32_t rc;
+    if (s.n < 1 || s.c < 1 || s.h < 1 || s.w < 1) return fail(-2, "l1_set: segment %d empty", k);
+    if ((rc = check_loss_tensor(s.a, "a")) || (rc = check_loss_tensor(s.b, "b"))) return rc;
+    if (bwd && s.da.data && (rc = check_loss_tensor(s.da, "da"))) return rc;
+  }
+  return 0;
+}
+
+extern "C" int32_t tpg_l1_set_fwd(int32_t nseg, const tpg_l1_seg* segs, float* ws, size_t ws_bytes, float* out,
+                                  tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc = check_l1_segs(nseg, segs, false);
+  if (rc) return rc;
+  if (!ws || ws_bytes < LOSS_WS || !out) return fail(-20, "l1_set: workspace / out");
+  return hip_check(launch_l1_set(nseg, segs, ws, nullptr, out, false, (hipStream_t)stream), "l1_set");
+}
+
+extern "C" int32_t tpg_l1_set_bwd(int32_t nseg, const tpg_l1_seg* segs, const float* gout, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc = check_l1_segs(nseg, segs, true);
+  if (rc) return rc;
+  if (!gout) return fail(-10, "l1_set: gout is NULL");
+  return hip_check(launch_l1_set(nseg, segs, nullptr, gout, nullptr, true, (hipStream_t)stream), "l1_set_bwd");
+}
+
 extern "C" int32_t tpg_act_bwd(int32_t n, int32_t c, int32_t h, int32_t w, int32_t act, float slope, tpg_tensor gy,
                                tpg_tensor y, tpg_tensor g, float* dbias, tpg_stream_t stream) {
   TPG_GROUP_SYNC();

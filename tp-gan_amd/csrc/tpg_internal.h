@@ -470,6 +470,12 @@ int launch_halo(const HaloArgs& a, int dtype, int cfg, hipStream_t s, bool mask 
 // pointwise (1x1) GEMM kernel on a one-tap halo plan (a.pw = tile config 1..4: 128x128, 128x64,
 // 64x128, 64x64 rows x output channels); same packed weights, epilogue and split-K slices
 int launch_pw(const HaloArgs& a, int dtype, hipStream_t s);
+// fused G-step losses (tpg_losses.hip): forward when dx / bwd is null / false (partials in part,
+// the scalar in out), else the gradient
+int launch_image_losses(int n, int c, int h, int w, const tpg_tensor& x, const tpg_tensor& r, float w_pix, float w_sym,
+                        float w_tv, float* part, const float* gout, float* out, const tpg_tensor* dx, hipStream_t st);
+int launch_l1_set(int nseg, const tpg_l1_seg* segs, float* part, const float* gout, float* out, bool bwd,
+                  hipStream_t st);
 int pw_tile_bm(int cfg);
 int pw_tile_bn(int cfg);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);

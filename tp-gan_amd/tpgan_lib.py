@@ -37,6 +37,13 @@ class ConvDesc(ctypes.Structure):
         ("data_algo", ctypes.c_int32)]
 
 
+class L1Seg(ctypes.Structure):  # tpg_l1_seg
+    _fields_ = [("n", ctypes.c_int32), ("c", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32),
+                ("a", TpgTensor), ("b", TpgTensor), ("da", TpgTensor), ("weight", ctypes.c_float)]
+
+
+L1_MAX_SEGS = 8
+
 FLAG_WPACKED = 1
 FLAG_CONCURRENT = 2
 FLAG_DX_ACCUM = 4
@@ -103,6 +110,14 @@ EXPORTS = {
                                                                    ctypes.POINTER(ctypes.c_int32),
                                                                    ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p,
                                                                    ctypes.c_int32, ctypes.c_void_p]),
+    "tpg_loss_workspace": (ctypes.c_size_t, []),
+    "tpg_image_losses_fwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor] + [ctypes.c_float] * 3 +
+                             [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_image_losses_bwd": (ctypes.c_int32, [ctypes.c_int32] * 4 + [TpgTensor, TpgTensor] + [ctypes.c_float] * 3 +
+                             [ctypes.c_void_p, TpgTensor, ctypes.c_void_p]),
+    "tpg_l1_set_fwd": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(L1Seg), ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_l1_set_bwd": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(L1Seg), ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_set_deterministic": (None, [ctypes.c_int32]),
     "tpg_group_begin": (None, []),
     "tpg_group_member": (None, []),

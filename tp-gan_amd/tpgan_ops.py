@@ -1369,6 +1369,105 @@ def cat(xs):
     return _Cat.apply(*xs)
 
 
+# ---- fused G-step image losses (tpg_losses.hip; tpgan_train._g_losses): one partial-sum and one
+# final launch forward, one launch backward, instead of ~100 aten launches on the critical path
+_LOSS_WS = {}
+
+
+def _loss_ws(device):
+    """The losses' partial-sum scratch (one per device; every loss launch is on the step's own
+    stream, in order)."""
+    ws = _LOSS_WS.get(device)
+    if ws is None:
+        ws = _LOSS_WS[device] = torch.empty(load().tpg_loss_workspace() // 4, dtype=torch.float32, device=device)
+    return ws
+
+
+def _grad_like(x):
+    n, c, h, w = x.shape
+    return new_act(n, c, h, w, x.dtype, x.device) if is_cl(x) else torch.empty_like(x, memory_format=torch.contiguous_format)
+
+
+class _ImageLosses(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, w_pix, w_sym, w_tv):
+        lib = load()
+        n, c, h, w = x.shape
+        if tuple(r.shape) != tuple(x.shape):
+            raise RuntimeError("image_losses: target %s != %s" % (tuple(r.shape), tuple(x.shape)))
+        ws = _loss_ws(x.device)
+        out = torch.empty((), dtype=torch.float32, device=x.device)
+        check(lib.tpg_image_losses_fwd(n, c, h, w, tt(x), tt(r), w_pix, w_sym, w_tv, ws.data_ptr(), ws.numel() * 4,
+                                       out.data_ptr(), stream_ptr()))
+        ctx.save_for_backward(x, r)
+        ctx.wts = (w_pix, w_sym, w_tv)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, r = ctx.saved_tensors
+        n, c, h, w = x.shape
+        g = g.float().contiguous()
+        dx = _grad_like(x)
+        check(load().tpg_image_losses_bwd(n, c, h, w, tt(x), tt(r), *ctx.wts, g.data_ptr(), tt(dx), stream_ptr()))
+        return dx, None, None, None, None
+
+
+def image_losses(x, target, w_pix, w_sym, w_tv):
+    """w_pix * mean|x - target| + w_sym * mean|x - flip_W(x)| + w_tv * (mean |vertical| + mean
+    |horizontal| neighbour differences of x), as one fp32 scalar (the G step's pixel,
+    symmetry and total-variation terms, tpgan_train._g_losses)."""
+    return _ImageLosses.apply(x, target, float(w_pix), float(w_sym), float(w_tv))
+
+
+class _L1Set(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weights, *ts):
+        from tpgan_lib import L1Seg
+        lib = load()
+        nseg = len(weights)
+        segs = (L1Seg * nseg)()
+        for k in range(nseg):
+            a, b = ts[2 * k], ts[2 * k + 1]
+            if tuple(a.shape) != tuple(b.shape) or a.dim() != 4:
+                raise RuntimeError("l1_means: pair %d shapes %s / %s" % (k, tuple(a.shape), tuple(b.shape)))
+            segs[k].n, segs[k].c, segs[k].h, segs[k].w = a.shape
+            segs[k].a, segs[k].b, segs[k].weight = tt(a), tt(b), float(weights[k])
+        ws = _loss_ws(ts[0].device)
+        out = torch.empty((), dtype=torch.float32, device=ts[0].device)
+        check(lib.tpg_l1_set_fwd(nseg, segs, ws.data_ptr(), ws.numel() * 4, out.data_ptr(), stream_ptr()))
+        ctx.save_for_backward(*ts)
+        ctx.weights = weights
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from tpgan_lib import L1Seg
+        ts = ctx.saved_tensors
+        nseg = len(ctx.weights)
+        segs = (L1Seg * nseg)()
+        grads = [None] * len(ts)
+        for k in range(nseg):
+            a, b = ts[2 * k], ts[2 * k + 1]
+            segs[k].n, segs[k].c, segs[k].h, segs[k].w = a.shape
+            segs[k].a, segs[k].b, segs[k].weight = tt(a), tt(b), float(ctx.weights[k])
+            if ctx.needs_input_grad[1 + 2 * k]:
+                grads[2 * k] = _grad_like(a)
+                segs[k].da = tt(grads[2 * k])
+        g = g.float().contiguous()
+        check(load().tpg_l1_set_bwd(nseg, segs, g.data_ptr(), stream_ptr()))
+        return (None,) + tuple(grads)
+
+
+def l1_means(pairs, weights):
+    """sum_i weights[i] * mean|a_i - b_i| over up to 8 (a_i, b_i) pairs of 4-D tensors, one fp32
+    scalar; gradients flow to the a_i (the G step's local-pathway pixel terms)."""
+    from tpgan_lib import L1_MAX_SEGS
+    if not 1 <= len(pairs) <= L1_MAX_SEGS or len(weights) != len(pairs):
+        raise ValueError("l1_means: 1..%d pairs with one weight each" % L1_MAX_SEGS)
+    return _L1Set.apply(tuple(float(w) for w in weights), *[t for p in pairs for t in p])
+
+
 class _LocalFuse(torch.autograd.Function):
     @staticmethod
     def forward(ctx, geom, *parts):

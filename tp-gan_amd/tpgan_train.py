@@ -441,6 +441,11 @@ def _hp_equal(a, b):
     return abs(float(a) - float(b)) <= 1e-12 * max(1.0, abs(float(b)))
 
 
+# the G step's pixel / symmetry / total-variation / local terms as the fused HIP ops
+# (tpgan_ops.image_losses / l1_means); False: the aten expressions (A/B, tests)
+FUSED_LOSSES = {"enabled": True}
+
+
 def total_variation(x):
     return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
 
@@ -643,17 +648,26 @@ class TPGANTrainer:
         """The G-step's pixel, local, symmetry, adversarial, total-variation and identity-class
         losses (build-defined, config.py:59-82 weights)."""
         w = self.w
-        f32 = fake.float()
-        l_pix = w["weight_128"] * (f32 - front).abs().mean()
-        l_local = ((le_f.float() - fle).abs().mean() + (re_f.float() - fre).abs().mean() +
-                   (no_f.float() - fno).abs().mean() + (mo_f.float() - fmo).abs().mean()) / 4.0
-        l_sym = (f32 - f32.flip(3)).abs().mean()
+        if not FUSED_LOSSES["enabled"]:  # (the aten form, A/B)
+            f32 = fake.float()
+            l_pix = w["weight_128"] * (f32 - front).abs().mean()
+            l_local = ((le_f.float() - fle).abs().mean() + (re_f.float() - fre).abs().mean() +
+                       (no_f.float() - fno).abs().mean() + (mo_f.float() - fmo).abs().mean()) / 4.0
+            l_sym = (f32 - f32.flip(3)).abs().mean()
+            return (w["weight_pixelwise"] * l_pix + w["weight_pixelwise_local"] * l_local +
+                    w["weight_symmetry"] * l_sym + w["weight_adv_G"] * -d_gen.mean() +
+                    w["weight_total_varation"] * total_variation(f32) +
+                    w["weight_cross_entropy"] * F.cross_entropy(pred.float(), label))
+        # w_pixelwise * w_128 * mean|fake - front| + w_symmetry * mean|fake - flip(fake)|
+        # + w_tv * total_variation(fake): one fused op (tpg_losses.hip), as the four local
+        # w_pixelwise_local * mean|patch - crop| / 4 terms
+        l_img = tpgan_ops.image_losses(fake, front, w["weight_pixelwise"] * w["weight_128"], w["weight_symmetry"],
+                                       w["weight_total_varation"])
+        l_local = tpgan_ops.l1_means([(le_f, fle), (re_f, fre), (no_f, fno), (mo_f, fmo)],
+                                     [w["weight_pixelwise_local"] / 4.0] * 4)
         l_adv = -d_gen.mean()
-        l_tv = total_variation(f32)
         l_ce = F.cross_entropy(pred.float(), label)
-        return (w["weight_pixelwise"] * l_pix + w["weight_pixelwise_local"] * l_local +
-                w["weight_symmetry"] * l_sym + w["weight_adv_G"] * l_adv + w["weight_total_varation"] * l_tv +
-                w["weight_cross_entropy"] * l_ce)
+        return l_img + l_local + w["weight_adv_G"] * l_adv + w["weight_cross_entropy"] * l_ce
 
     def _phase_c(self, b):
         with tpgan_ops.roctx_range("G-adam"):
