@@ -27,9 +27,10 @@ __global__ __launch_bounds__(NW * 64) void loop_kernel(int taps, float* out, con
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
-  u32x4* A = lds;              // halo: 1024 rows x 4 chunks (64 KiB)
-  u32x4* B = lds + 4096;       // 3 slots x 256 rows x 4 chunks (48 KiB)
-  for (int i = tid; i < 4096 + 3072; i += NW * 64) lds[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
+  constexpr int AR = NW * 128;  // halo rows: 1024 (8 waves, 64 KiB) / 512 (4 waves, 32 KiB)
+  u32x4* A = lds;
+  u32x4* B = lds + AR * 4;     // 3 slots x 256 rows x 4 chunks (48 KiB)
+  for (int i = tid; i < AR * 4 + 3072; i += NW * 64) lds[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
   __syncthreads();
   f32x4 acc[MREP][NREP];
 #pragma unroll
@@ -48,7 +49,7 @@ __global__ __launch_bounds__(NW * 64) void loop_kernel(int taps, float* out, con
     const int shift = (t % 5) + 68 * ((t / 5) % 5);
 #pragma unroll
     for (int m = 0; m < MREP; ++m) {
-      const int hp = (wave * MREP * 16 + m * 16 + l16 + shift) & 1023;
+      const int hp = (wave * MREP * 16 + m * 16 + l16 + shift) & (AR - 1);
       xa[set][m] = A[hp * 4 + (g ^ (((hp >> 2) & 1) << 1))];
     }
 #pragma unroll
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(NW * 64) void loop_kernel(int taps, float* out, con
       u32x4 af[MREP], bf[NREP];
 #pragma unroll
       for (int m = 0; m < MREP; ++m) {
-        const int hp = (wave * MREP * 16 + m * 16 + l16 + shift) & 1023;
+        const int hp = (wave * MREP * 16 + m * 16 + l16 + shift) & (AR - 1);
         af[m] = A[hp * 4 + (g ^ (((hp >> 2) & 1) << 1))];
       }
 #pragma unroll
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(NW * 64) void loop_kernel(int taps, float* out, con
       u32x4 af[MREP], bf[NREP];
 #pragma unroll
       for (int m = 0; m < MREP; ++m) {
-        const int hp = (wave * MREP * 16 + m * 16 + l16 + shift) & 1023;
+        const int hp = (wave * MREP * 16 + m * 16 + l16 + shift) & (AR - 1);
         const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)(A + hp * 4 + (g ^ (((hp >> 2) & 1) << 1)));
         asm volatile("ds_read_b128 %0, %1" : "=v"(af[m]) : "v"(a));
       }
@@ -185,12 +186,12 @@ __global__ __launch_bounds__(NW * 64) void loop_kernel(int taps, float* out, con
   out[blockIdx.x * 512 + tid] = s;  // (NW <= 8)
 }
 
-template <int MREP, int NREP, int MODE, int BARP, int DMA = 0, int NW = 8>
+template <int MREP, int NREP, int MODE, int BARP, int DMA = 0, int NW = 8, int BPC = 1>
 static int run(const char* name, float* out, int taps, hipEvent_t e0, hipEvent_t e1, const char* w) {
   auto k = loop_kernel<MREP, NREP, MODE, BARP, DMA, NW>;
-  const int lds = 150 * 1024;  // one block per CU
+  const int lds = (BPC == 1 ? 150 : 80) * 1024;  // one (or two: 2 x 80 KiB = the CU's 160) blocks per CU
   CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  const int blocks = 256 * 4;
+  const int blocks = 256 * 4 * BPC;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(NW * 64), lds, 0, taps, out, w);
   CHECK(hipEventRecord(e0));
   hipLaunchKernelGGL(k, dim3(blocks), dim3(NW * 64), lds, 0, taps, out, w);
@@ -199,14 +200,14 @@ static int run(const char* name, float* out, int taps, hipEvent_t e0, hipEvent_t
   float ms;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   const double flops = 2.0 * 16 * 16 * 32 * MREP * NREP * (double)NW * taps * blocks;
-  printf("%-26s %dw bar/%d dma %d MREP %d NREP %2d  %.3f ms  %.0f TF/s  %.1f %% of 2.5 PF\n", name, NW, BARP, DMA, MREP, NREP, ms, flops / ms / 1e9,
+  printf("%-26s %dw x%d bar/%d dma %d MREP %d NREP %2d  %.3f ms  %.0f TF/s  %.1f %% of 2.5 PF\n", name, NW, BPC, BARP, DMA, MREP, NREP, ms, flops / ms / 1e9,
          flops / ms / 1e9 / 25.0);
   return 0;
 }
 
 int main() {
   float* out;
-  CHECK(hipMalloc(&out, 256 * 4 * 512 * 4));
+  CHECK(hipMalloc(&out, 256 * 4 * 2 * 512 * 4));  // (up to 2 blocks per CU x 512 threads)
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -214,6 +215,14 @@ int main() {
   char* w;
   CHECK(hipMalloc(&w, 64 * 16384 + 65536));
   CHECK(hipMemset(w, 0, 64 * 16384 + 65536));
+  // two 4-wave blocks per CU (each with its own barrier) against one 8-wave block
+  run<2, 13, 0, 1, 2, 8, 1>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<2, 13, 0, 1, 4, 4, 2>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<2, 13, 0, 1, 0, 4, 2>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<2, 13, 0, 0, 0, 4, 2>("lds all-then-mfma", out, taps, e0, e1, w);
+  run<2, 13, 3, 1, 4, 4, 2>("prefetch next tap", out, taps, e0, e1, w);
+  run<2, 13, 4, 1, 4, 4, 2>("prefetch interleaved", out, taps, e0, e1, w);
+  run<2, 13, 1, 1, 0, 4, 2>("regs only", out, taps, e0, e1, w);
   run<2, 13, 1, 1>("regs only", out, taps, e0, e1, w);
   run<4, 7, 1, 1, 0, 4>("regs only", out, taps, e0, e1, w);
   run<4, 7, 0, 1, 0, 4>("lds all-then-mfma", out, taps, e0, e1, w);
