@@ -1024,6 +1024,12 @@ class _ConvWgrad(torch.autograd.Function):
 
 def _conv_act_backward_graph(ctx, gy):
     x, weight, y = ctx.saved_tensors
+    wp = ctx.wparam
+    if wp is not None and weight is not wp and wp.requires_grad:
+        # a view of the parameter (tap-folded / reshaped weight): the same view taken again now,
+        # so that it is connected to the parameter even when the forward ran with the parameter
+        # frozen (the WGAN-GP first-order pass; the old view then has no gradient edge)
+        weight = wp.as_strided(weight.shape, weight.stride(), weight.storage_offset())
     d = _plain_desc(ctx.d)
     g = _ActMask.apply(gy, y, ctx.d.act, ctx.d.slope)
     dx = dw = dbias = dres = None

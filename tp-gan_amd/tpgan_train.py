@@ -478,6 +478,7 @@ class TPGANTrainer:
         self.dtype = compute_dtype
         self.w = dict(LOSS_W if loss_weights is None else loss_weights)
         self.gp = gradient_penalty
+        self.gp_frozen_first_order = True  # (gradient_penalty: D frozen in the first-order pass; False = A/B)
         self.sync = GradSync(process_group)
         self.world = self.sync.world
         # G's 551 MB of gradients are reduced bucket by bucket during the G backward, D's 54 MB
@@ -609,7 +610,18 @@ class TPGANTrainer:
         B = real.shape[0]
         a = torch.rand(B, 1, 1, 1, device=real.device, dtype=torch.float32) if alpha is None else alpha
         x_hat = (a * real.float() + (1 - a) * fake.float()).requires_grad_(True)
-        d_hat = self.D(x_hat).float()
+        # D's parameters are frozen for this forward, so the first-order pass (grad w.r.t. x_hat
+        # only) skips every weight / bias gradient it would otherwise compute and discard; they
+        # require grad again before the graph of gx is built, so gx's own nodes (the input
+        # gradients, which read the saved weights) carry the double backward to them
+        params = [p for p in self.D.parameters()] if self.gp_frozen_first_order else []
+        flags = [p.requires_grad for p in params]
+        set_requires_grad(params, False)
+        try:
+            d_hat = self.D(x_hat).float()
+        finally:
+            for p, f in zip(params, flags):
+                p.requires_grad_(f)
         (gx,) = torch.autograd.grad(d_hat.sum(), x_hat, create_graph=True)
         return ((gx.reshape(B, -1).float().norm(dim=1) - 1.0) ** 2).mean()
 
