@@ -441,6 +441,10 @@ def _hp_equal(a, b):
     return abs(float(a) - float(b)) <= 1e-12 * max(1.0, abs(float(b)))
 
 
+# the first train step runs the local pathways ungrouped so that their shapes are autotuned
+# (a grouped launch cannot time candidates); False: grouped from the first step (A/B)
+TUNE_UNGROUPED = {"enabled": True}
+
 # the G step's pixel / symmetry / total-variation / local terms as the fused HIP ops
 # (tpgan_ops.image_losses / l1_means); False: the aten expressions (A/B, tests)
 FUSED_LOSSES = {"enabled": True}
@@ -479,6 +483,7 @@ class TPGANTrainer:
         self.w = dict(LOSS_W if loss_weights is None else loss_weights)
         self.gp = gradient_penalty
         self.gp_frozen_first_order = True  # (gradient_penalty: D frozen in the first-order pass; False = A/B)
+        self._tuned_ungrouped = False
         self.sync = GradSync(process_group)
         self.world = self.sync.world
         # G's 551 MB of gradients are reduced bucket by bucket during the G backward, D's 54 MB
@@ -781,6 +786,17 @@ class TPGANTrainer:
     def step(self, b, next_b=None):
         """One eager G+D train step.  next_b: the batch of the following step, when known --
         its D(real) pass then runs under this step's G-gradient all-reduce tail (real_ahead)."""
+        if not self._tuned_ungrouped and TUNE_UNGROUPED["enabled"] and tpgan_ops.AUTOTUNE["enabled"]:
+            # the first step runs the local pathways ungrouped (their own streams, same
+            # concurrency flag), so the weight-gradient tuner sees their shapes; the grouped
+            # launches of later steps take those picks from the tuning cache
+            self._tuned_ungrouped = True
+            prev = tpgan_ops.GROUP["enabled"]
+            tpgan_ops.GROUP["enabled"] = False
+            try:
+                return self.step(b, next_b)
+            finally:
+                tpgan_ops.GROUP["enabled"] = prev
         self._phase_a(b)
         with tpgan_ops.roctx_range("allreduce-D"):
             self._allreduce(self.fD)
