@@ -4,7 +4,7 @@ process, one trainer, variants alternated round by round: cdna_hip_programming.m
     python tools/ab_step.py [--steps 10] [--rounds 5] VARIANT [VARIANT ...]
 
 VARIANT = name[:module.ATTR[.key]=value,...], e.g.
-    base   side:tpgan_ops.WGRAD_SIDE.enabled=1   nogroup:tpgan_ops.GROUP.enabled=0
+    base   side:tpgan_ops.WGRAD_SIDE.enabled=1   nogroup:tpgan_ops.GROUP.enabled=0   nt:env.TPG_OPT_VAR=3
 Values are parsed as int / float / bool literals.  Prints per-variant median and min ms/step.
 """
 import argparse
@@ -32,6 +32,9 @@ def parse_variant(spec):
             prio = int(val)
             continue
         parts = path.split(".")
+        if parts[0] == "env":  # env.NAME=value: an environment variable the library reads per launch
+            sets.append(("env", [parts[1]], val))
+            continue
         mod = TRAINER if parts[0] == "trainer" else importlib.import_module(parts[0])
         lv = val.lower()
         if lv in ("true", "false", "none"):
@@ -45,6 +48,10 @@ def parse_variant(spec):
 def apply(sets):
     old = []
     for mod, attrs, v in sets:
+        if mod == "env":
+            old.append(("env", attrs[0], os.environ.get(attrs[0]), None))
+            os.environ[attrs[0]] = v
+            continue
         obj = TRAINER[0] if mod is TRAINER else mod
         for a in attrs[:-1]:
             obj = getattr(obj, a) if not isinstance(obj, dict) else obj[a]
@@ -60,7 +67,12 @@ def apply(sets):
 
 def restore(old):
     for obj, last, v, is_dict in reversed(old):
-        if is_dict:
+        if obj == "env":
+            if v is None:
+                os.environ.pop(last, None)
+            else:
+                os.environ[last] = v
+        elif is_dict:
             obj[last] = v
         else:
             setattr(obj, last, v)

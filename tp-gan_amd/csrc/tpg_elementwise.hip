@@ -36,6 +36,45 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs p, int nthread
   if (idx < nthreads) pack_igemm_item<E>(p, idx);
 }
 
+// Halo-layout image whose packed rows n' run along the weight's unit-stride channel and whose
+// chunks run along a strided one (the input-gradient images of channels-last weights): the
+// block's 64 rows x ROW channels are read as unit-stride runs (one 256-byte run per wave and
+// load), transposed through LDS and written as the item kernel's 16-byte chunks.
+template <typename E>
+__device__ __forceinline__ void pack_halo_block_t(const PackArgs& p, int bn, int bnl, int ntiles, int lb) {
+  constexpr int EPC = 16 / sizeof(E);
+  constexpr int ROW = 4 * EPC;
+  __shared__ float tile[ROW][65];
+  const int t = threadIdx.x;
+  int rr = lb * 64 / bnl;           // (bnl is a multiple of 128: the block's rows share one (ks, tap, nt))
+  const int r0 = lb * 64 - rr * bnl;
+  const int nt = rr % ntiles;
+  rr /= ntiles;
+  const int tap = rr % p.ntaps;
+  const int ks = rr / p.ntaps;
+  const int64_t tapoff = (int64_t)p.tr[tap] * p.w_sr + (int64_t)p.ts[tap] * p.w_ss;
+  {
+    const int rl = t & 63;
+    const int r = r0 + rl;
+    const int np = nt * bn + r;
+    const bool row_ok = r < bn && np < p.Nreal;
+    const float* src = p.W + tapoff + np;
+#pragma unroll
+    for (int e = 0; e < ROW / 4; ++e) {
+      const int cl = (t >> 6) * (ROW / 4) + e;
+      const int c = ks * ROW + cl;
+      tile[cl][rl] = (row_ok && c < p.Creal) ? src[(int64_t)c * p.w_sa] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int rl = t >> 2, pchunk = t & 3;
+  const int cl0 = (pchunk ^ pack_hswz(r0 + rl)) * EPC;
+  union { uint4 u; E e[EPC]; } o;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) o.e[e] = (E)tile[cl0 + e][rl];
+  reinterpret_cast<uint4*>(p.Wp)[(int64_t)lb * 256 + t] = o.u;
+}
+
 // Every weight pack of a network in one launch: block b finds its job (binary search over
 // first_block), stages the job in LDS and packs items (b - first_block)*256 + tid.
 __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restrict__ jobs, int n) {
@@ -57,7 +96,15 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restric
     for (int i = threadIdx.x; i < (int)(sizeof(PackJob) / 4); i += 256) dst[i] = src[i];
   }
   __syncthreads();
-  const int idx = (blockIdx.x - job.first_block) * 256 + threadIdx.x;
+  const int lb = blockIdx.x - job.first_block;
+  const int idx = lb * 256 + threadIdx.x;
+  if (job.kind == 1 && job.k.cmode == 0 && job.k.nmode == 1 && job.k.w_sb == 1) {
+    // (block-uniform: items is a multiple of 256, bnl of 128)
+    if (job.k.dtype == TPG_BF16) pack_halo_block_t<__bf16>(job.k, job.bn, job.bnl, job.ntiles, lb);
+    else if (job.k.dtype == TPG_F16) pack_halo_block_t<_Float16>(job.k, job.bn, job.bnl, job.ntiles, lb);
+    else pack_halo_block_t<float>(job.k, job.bn, job.bnl, job.ntiles, lb);
+    return;
+  }
   if (idx >= job.items) return;
   if (job.kind == 1) {
     if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx);
@@ -550,9 +597,24 @@ __device__ __forceinline__ void adam_one(float& pv, float g, float gscale, float
   pv = pv - lr_bc1 * mv / (sqrtf(vv) / bc2s + eps);
 }
 
+typedef float tpg_f4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ tpg_f4 adam_ld(const float* p, int64_t i) {
+  const tpg_f4* q = reinterpret_cast<const tpg_f4*>(p) + i;
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void adam_st(float* p, int64_t i, tpg_f4 v) {
+  tpg_f4* q = reinterpret_cast<tpg_f4*>(p) + i;
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
 // head: elements before the first 16-byte boundary (a bucket slice of the flat buffers starts
 // wherever its first parameter does; all four buffers share the misalignment), updated one per
-// thread by block 0; the rest from p + head on in float4s
+// thread by block 0; the rest from p + head on in float4s (U of each operand in flight per thread)
+template <bool NT, int U>
 __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ gr,
                                                    float* __restrict__ m, float* __restrict__ v, float lr, float b1,
                                                    float b2, float eps, float wd, const float* __restrict__ st,
@@ -566,40 +628,40 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
   }
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // two float4 of each operand per thread and iteration: eight 16-byte loads in flight
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  for (; i + stride < n4; i += 2 * stride) {
-    float4 pv[2], g[2], mv[2], vv[2];
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    tpg_f4 pv[U], g[U], mv[U], vv[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      pv[u] = reinterpret_cast<float4*>(p)[i + u * stride];
-      g[u] = reinterpret_cast<const float4*>(gr)[i + u * stride];
-      mv[u] = reinterpret_cast<float4*>(m)[i + u * stride];
-      vv[u] = reinterpret_cast<float4*>(v)[i + u * stride];
+    for (int u = 0; u < U; ++u) {
+      pv[u] = adam_ld<NT>(p, i + u * stride);
+      g[u] = adam_ld<NT>(gr, i + u * stride);
+      mv[u] = adam_ld<NT>(m, i + u * stride);
+      vv[u] = adam_ld<NT>(v, i + u * stride);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      adam_one(pv[u].x, g[u].x, gscale, mv[u].x, vv[u].x, lr_bc1, b1, b2, eps, wd, bc2s);
-      adam_one(pv[u].y, g[u].y, gscale, mv[u].y, vv[u].y, lr_bc1, b1, b2, eps, wd, bc2s);
-      adam_one(pv[u].z, g[u].z, gscale, mv[u].z, vv[u].z, lr_bc1, b1, b2, eps, wd, bc2s);
-      adam_one(pv[u].w, g[u].w, gscale, mv[u].w, vv[u].w, lr_bc1, b1, b2, eps, wd, bc2s);
-      reinterpret_cast<float4*>(p)[i + u * stride] = pv[u];
-      reinterpret_cast<float4*>(m)[i + u * stride] = mv[u];
-      reinterpret_cast<float4*>(v)[i + u * stride] = vv[u];
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = pv[u][e], me = mv[u][e], ve = vv[u][e];
+        adam_one(pe, g[u][e], gscale, me, ve, lr_bc1, b1, b2, eps, wd, bc2s);
+        pv[u][e] = pe; mv[u][e] = me; vv[u][e] = ve;
+      }
+      adam_st<NT>(p, i + u * stride, pv[u]);
+      adam_st<NT>(m, i + u * stride, mv[u]);
+      adam_st<NT>(v, i + u * stride, vv[u]);
     }
   }
   for (; i < n4; i += stride) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    const float4 g = reinterpret_cast<const float4*>(gr)[i];
-    float4 mv = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam_one(pv.x, g.x, gscale, mv.x, vv.x, lr_bc1, b1, b2, eps, wd, bc2s);
-    adam_one(pv.y, g.y, gscale, mv.y, vv.y, lr_bc1, b1, b2, eps, wd, bc2s);
-    adam_one(pv.z, g.z, gscale, mv.z, vv.z, lr_bc1, b1, b2, eps, wd, bc2s);
-    adam_one(pv.w, g.w, gscale, mv.w, vv.w, lr_bc1, b1, b2, eps, wd, bc2s);
-    reinterpret_cast<float4*>(p)[i] = pv;
-    reinterpret_cast<float4*>(m)[i] = mv;
-    reinterpret_cast<float4*>(v)[i] = vv;
+    tpg_f4 pv = adam_ld<NT>(p, i), g = adam_ld<NT>(gr, i), mv = adam_ld<NT>(m, i), vv = adam_ld<NT>(v, i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pv[e], me = mv[e], ve = vv[e];
+      adam_one(pe, g[e], gscale, me, ve, lr_bc1, b1, b2, eps, wd, bc2s);
+      pv[e] = pe; mv[e] = me; vv[e] = ve;
+    }
+    adam_st<NT>(p, i, pv);
+    adam_st<NT>(m, i, mv);
+    adam_st<NT>(v, i, vv);
   }
   for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
     adam_one(p[i], gr[i], gscale, m[i], v[i], lr_bc1, b1, b2, eps, wd, bc2s);
@@ -803,9 +865,12 @@ extern "C" int32_t tpg_adam_impl(int64_t numel, float* param, const float* grad,
   if (host_step >= 0) hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, state, b1, b2, host_step);
   if (numel <= 0) return (int)hipGetLastError();
   const int head = (int)std::min<int64_t>(numel, mis ? (int64_t)((16 - mis) / 4) : 0);
-  int blocks = (int)std::min<int64_t>(((numel - head) / 4 + 255) / 256, 4096);
+  // (nontemporal loads / stores, up to 64 Ki blocks: 0.85 -> 0.71 ms for G's 138 M parameters,
+  // 4.5 -> 5.4 TB/s; the step 32.44 -> 32.34 ms, profiles/r04/ab_adam_pack.txt)
+  int blocks = (int)std::min<int64_t>(((numel - head) / 4 + 255) / 256, 65536);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, state,
+  auto k = adam_kernel<true, 2>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, s, numel, param, grad, m, v, lr, b1, b2, eps, wd, state,
                      gscale, head);
   return (int)hipGetLastError();
 }
