@@ -950,7 +950,7 @@ extern "C" int32_t tpg_conv2d_pack_jobs(const tpg_conv_desc* d, int32_t op, tpg_
         j.kind = 0;
         j.items = j.k.Npad * j.k.nunits;
       }
-      j.nblocks = cdiv(j.items, 256);
+      j.nblocks = cdiv(j.items, 256 * TPG_PACK_GROUPS);
     }
     off += region;
   }

@@ -76,7 +76,9 @@ __device__ __forceinline__ void pack_halo_block_t(const PackArgs& p, int bn, int
 }
 
 // Every weight pack of a network in one launch: block b finds its job (binary search over
-// first_block), stages the job in LDS and packs items (b - first_block)*256 + tid.
+// first_block), stages the job in LDS and packs TPG_PACK_GROUPS groups of 256 items,
+// ((b - first_block)*TPG_PACK_GROUPS + g)*256 + tid (one group per block measured latency-bound
+// on the search and the job copy: 150 k blocks for G's images).
 __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restrict__ jobs, int n) {
   __shared__ PackJob job;
   __shared__ int jsel;
@@ -96,24 +98,30 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restric
     for (int i = threadIdx.x; i < (int)(sizeof(PackJob) / 4); i += 256) dst[i] = src[i];
   }
   __syncthreads();
-  const int lb = blockIdx.x - job.first_block;
-  const int idx = lb * 256 + threadIdx.x;
+  const int lb0 = (blockIdx.x - job.first_block) * TPG_PACK_GROUPS;
   if (job.kind == 1 && job.k.cmode == 0 && job.k.nmode == 1 && job.k.w_sb == 1) {
     // (block-uniform: items is a multiple of 256, bnl of 128)
-    if (job.k.dtype == TPG_BF16) pack_halo_block_t<__bf16>(job.k, job.bn, job.bnl, job.ntiles, lb);
-    else if (job.k.dtype == TPG_F16) pack_halo_block_t<_Float16>(job.k, job.bn, job.bnl, job.ntiles, lb);
-    else pack_halo_block_t<float>(job.k, job.bn, job.bnl, job.ntiles, lb);
+    for (int lb = lb0; lb < lb0 + TPG_PACK_GROUPS && lb * 256 < job.items; ++lb) {
+      if (job.k.dtype == TPG_BF16) pack_halo_block_t<__bf16>(job.k, job.bn, job.bnl, job.ntiles, lb);
+      else if (job.k.dtype == TPG_F16) pack_halo_block_t<_Float16>(job.k, job.bn, job.bnl, job.ntiles, lb);
+      else pack_halo_block_t<float>(job.k, job.bn, job.bnl, job.ntiles, lb);
+      __syncthreads();  // (the LDS tile is refilled by the next group)
+    }
     return;
   }
-  if (idx >= job.items) return;
-  if (job.kind == 1) {
-    if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx);
-    else if (job.k.dtype == TPG_F16) pack_halo_item<_Float16>(job.k, job.bn, job.bnl, job.ntiles, idx);
-    else pack_halo_item<float>(job.k, job.bn, job.bnl, job.ntiles, idx);
-  } else {
-    if (job.k.dtype == TPG_BF16) pack_igemm_item<__bf16>(job.k, idx);
-    else if (job.k.dtype == TPG_F16) pack_igemm_item<_Float16>(job.k, idx);
-    else pack_igemm_item<float>(job.k, idx);
+#pragma unroll 1
+  for (int g = 0; g < TPG_PACK_GROUPS; ++g) {
+    const int idx = (lb0 + g) * 256 + threadIdx.x;
+    if (idx >= job.items) break;
+    if (job.kind == 1) {
+      if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx);
+      else if (job.k.dtype == TPG_F16) pack_halo_item<_Float16>(job.k, job.bn, job.bnl, job.ntiles, idx);
+      else pack_halo_item<float>(job.k, job.bn, job.bnl, job.ntiles, idx);
+    } else {
+      if (job.k.dtype == TPG_BF16) pack_igemm_item<__bf16>(job.k, idx);
+      else if (job.k.dtype == TPG_F16) pack_igemm_item<_Float16>(job.k, idx);
+      else pack_igemm_item<float>(job.k, idx);
+    }
   }
 }
 

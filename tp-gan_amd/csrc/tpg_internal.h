@@ -236,15 +236,17 @@ struct PackArgs {
   int8_t tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
 };
 
-// Batched weight packing (tpg_pack_run): one job per packed problem.  Jobs start on
-// 256-item boundaries (`first_block`), so every block of the batch kernel packs for
+constexpr int TPG_PACK_GROUPS = 8;  // 256-item groups per block of the batched pack kernel
+
+// Batched weight packing (tpg_pack_run): one job per packed problem.  Jobs start on block
+// boundaries (`first_block`, TPG_PACK_GROUPS * 256 items), so every block packs for
 // exactly one job.
 struct PackJob {
   PackArgs k;
   int kind;                   // 0: implicit-GEMM layout (pack_kernel), 1: halo layout (pack_halo_kernel)
   int nks, bn, bnl, ntiles;   // halo layout
   int items;                  // igemm: Npad * nunits 16-element units; halo: 16-byte chunks
-  int first_block;            // set by tpg_pack_prepare
+  int first_block;            // set by tpg_pack_prepare (blocks of TPG_PACK_GROUPS * 256 items)
   int nblocks;
 };
 
