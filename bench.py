@@ -151,6 +151,8 @@ def main():
         tpgan_ops.PROBE["match"] = match
         tpgan_ops.PROBE["events"] = []
     if world > 1:
+        trainer.comm_timing = True  # exposed-communication events around each exchange (timed steps only)
+        trainer.comm_events = []
         dist.barrier()
     torch.cuda.synchronize()
     # per-step HIP events on the launching stream (every step ends on it: side streams join)
@@ -168,6 +170,14 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    exposed = None
+    if world > 1:
+        trainer.comm_timing = False
+        exposed = trainer.exposed_comm_ms()
+        # max over ranks, like the step time (the slowest rank's wait is the one that costs)
+        ex = torch.tensor([exposed["G"], exposed["D"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        exposed["G"], exposed["D"] = float(ex[0]), float(ex[1])
     ms_per_step = elapsed / args.steps * 1e3
     faces = world * B * args.steps / elapsed
     step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
@@ -219,7 +229,10 @@ def main():
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count()
             r = time_cpu_step(B=cb, iters=args.cpu_iters, threads=threads)
             cpu = {"value": round(r["full_fps"], 4), "unit": "faces/s", "cores": r["threads"], "threads": r["threads"],
-                   "host_cpu_count": os.cpu_count(), "kind": "port", "cpu_model": r["cpu"],
+                   "host_cpu_count": os.cpu_count(),
+                   "cores_meaning": "threads this process used (its CPU share on the box: OMP_NUM_THREADS, else "
+                                    "os.cpu_count()), not the host's core count (host_cpu_count)",
+                   "kind": "port", "cpu_model": r["cpu"],
                    "sample": "oracle/cpu_step.py full G+D train step incl. both Adam updates, 128x128, B=%d, fp32 "
                              "aten CPU, 1 warm-up + median of %d steps (%.2f s/step)" % (cb, args.cpu_iters,
                                                                                         r["full_s"]),
@@ -293,10 +306,19 @@ def main():
         "cpu_baseline": cpu,
     }
     if world > 1:
+        bst = trainer.bucket_stats()
+        n_ex = max(exposed["steps"], 1)
         out["dp"] = {"backend": args.dist_backend, "devices": ndev,
                      "real_ahead_reused": trainer.real_ahead_used,
-                     "g_buckets": len(trainer.gsync.buckets) if trainer.gsync is not None else 0,
-                     "d_buckets": len(trainer.dsync.buckets) if trainer.dsync is not None else 0,
+                     "g_buckets": bst["G"]["buckets"], "d_buckets": bst["D"]["buckets"],
+                     "g_bucket_bytes": bst["G"]["bytes"], "d_bucket_bytes": bst["D"]["bytes"],
+                     "buckets": bst,
+                     "exposed_comm_ms_per_step": {
+                         "G": round(exposed["G"] / n_ex, 4), "D": round(exposed["D"] / n_ex, 4),
+                         "total": round((exposed["G"] + exposed["D"]) / n_ex, 4), "steps": exposed["steps"],
+                         "source": "HIP events on the compute stream around each gradient exchange (bucket tail "
+                                   "wait + any un-overlapped all-reduce), max over ranks"},
+                     "overlap_optimizer": trainer.overlap_optimizer,
                      "bucket_order_learned": bool(trainer.gsync is not None and trainer.gsync.order_learned)}
     print(json.dumps(out))
     if world > 1:

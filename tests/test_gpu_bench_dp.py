@@ -54,3 +54,15 @@ def test_bench_torchrun_two_ranks_one_gpu(gpu):
     # every step after the first reuses the D(real) pass the previous one ran under G's tail
     assert dp["real_ahead_reused"] >= 2, dp
     assert dp["g_buckets"] > 1 and dp["d_buckets"] >= 1 and dp["bucket_order_learned"], dp
+    # what the first 8-GPU run needs to show where scaling is lost -- bucket
+    # counts and bytes of both exchanges, and the communication time the compute stream waited for
+    b = dp["buckets"]
+    assert b["G"]["buckets"] == dp["g_buckets"] and b["D"]["buckets"] == dp["d_buckets"], b
+    assert b["G"]["bytes"] == dp["g_bucket_bytes"] > 500e6 and b["D"]["bytes"] == dp["d_bucket_bytes"] > 50e6, b
+    assert b["G"]["min_bucket_bytes"] <= b["G"]["max_bucket_bytes"] and b["G"]["overlapped"], b
+    ex = dp["exposed_comm_ms_per_step"]
+    assert ex["steps"] == 2, ex
+    assert ex["G"] >= 0 and ex["D"] >= 0 and abs(ex["total"] - ex["G"] - ex["D"]) < 1e-3, ex
+    # (gloo on one shared GPU: the host-side waits are real, so some exposure is measured)
+    assert ex["total"] > 0, ex
+    assert dp["overlap_optimizer"] is False

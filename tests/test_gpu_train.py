@@ -182,7 +182,53 @@ def test_graph_replay_matches_eager(gpu, segmented):
         _graph_case(gpu, segmented)
 
 
-def _graph_case(gpu, segmented):
+class _Cycle:
+    """A reference cycle that owns device memory (what a dropped trainer <-> gradient-sync
+    pair was in round 4): freed only by the cyclic garbage collector."""
+
+    def __init__(self, gpu):
+        self.t = torch.empty(1 << 20, device=gpu)
+        self.me = self
+
+
+def test_graph_capture_gc_safe(gpu):
+    """a cyclic collection inside the capture window freed device memory
+    mid-capture and aborted the process.  Here a device-memory cycle becomes garbage at the
+    start of phase B -- inside the capture -- with the collector's threshold at 1, so any
+    allocation of Python objects would collect it there; capture() keeps the collector off
+    for the window, the capture completes, and the replays still match eager steps bit for bit
+    (deterministic mode).  The cycle is collected once the capture has ended."""
+    import gc
+    import weakref
+    import tpgan_ops
+    holder = {"c": _Cycle(gpu)}
+    probe = weakref.ref(holder["c"])
+    seen = {}
+
+    def arm(tr):
+        orig = tr._phase_b
+
+        def phase_b(b):
+            if tr._capturing and "c" in holder:
+                del holder["c"]              # unreachable now, but for the cycle
+                seen["gc_enabled"] = gc.isenabled()
+                seen["alive_in_capture"] = probe() is not None
+            return orig(b)
+        tr._phase_b = phase_b
+
+    thr = gc.get_threshold()
+    gc.set_threshold(1, 1, 1)
+    try:
+        with tpgan_ops.deterministic():
+            _graph_case(gpu, False, arm=arm)
+    finally:
+        gc.set_threshold(*thr)
+    assert seen == {"gc_enabled": False, "alive_in_capture": True}, seen
+    gc.collect()
+    assert probe() is None
+
+
+def _graph_case(gpu, segmented, arm=None):
     import tpgan_train
     G, D = _models(gpu)
     tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False)
@@ -190,6 +236,8 @@ def _graph_case(gpu, segmented):
     tr.step(b)  # autotune outside capture
     torch.cuda.synchronize()
     snap = _snapshot(tr)
+    if arm is not None:
+        arm(tr)
 
     def two_eager():
         _restore(tr, snap)

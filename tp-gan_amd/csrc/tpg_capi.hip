@@ -206,7 +206,15 @@ static GLaunch& grec(int kind, hipStream_t s, int dtype) {
 static int do_halo(const HaloArgs& h, int dtype, int cfg, hipStream_t s, bool mask) {
   if (h.pw > 0 && !mask) {  // (not a launch-group kernel: the recorded launches go first)
     const int rc = group_flush();
-    return rc ? rc : launch_pw(h, dtype, s);
+    if (rc) return rc;
+    const int e = launch_pw(h, dtype, s);
+    if (e != -1) return e;
+    // the pointwise kernel refused the plan (its 32-bit byte-extent / stride conditions are
+    // stricter than the planner's element-count checks): the halo kernel of the same plan and
+    // packed weight image takes it
+    HaloArgs h2 = h;
+    h2.pw = 0;
+    return launch_halo(h2, dtype, cfg, s, false);
   }
   if (!g_grp.active) return launch_halo(h, dtype, cfg, s, mask);
   GLaunch& L = grec(1, s, dtype);

@@ -311,7 +311,9 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
       // (the four halves are taken apart as scalars: this hipcc compiles
       // __builtin_bit_cast(E, vec[u]) of an ext_vector element as element 0 for every u --
       // the parked round-3 version of this path read the first residual four times)
-      if (((yo | (R ? ro : 0)) & 3) == 0) {
+      // (the base pointers too: a channel-offset view through the public C API may start on
+      // any 2-byte boundary)
+      if (((yo | (R ? ro : 0)) & 3) == 0 && (((uintptr_t)Y | (uintptr_t)R) & 7) == 0) {
         uint2 rw = make_uint2(0u, 0u);
         if (R) rw = *reinterpret_cast<const uint2*>(R + ro);
         uint32_t ow[2];

@@ -274,7 +274,10 @@ class ConvGeom:
 # tpg_conv2d_bwd_filter are chosen per shape on first use by timing every candidate into a
 # scratch gradient (HIP events, device synchronised around each trial, so only during
 # warm-up).  bf16 only; the cache can be saved / loaded as JSON for reproducible runs.
-AUTOTUNE = {"enabled": True, "cache": {}, "trials": 0}
+# frozen: shapes first seen now take the planner's default plan instead of being timed (a
+# trainer closes the tuning window after its first steps, so a later new shape -- a partial
+# last batch -- does not stop the device for a tuning sweep in the middle of training)
+AUTOTUNE = {"enabled": True, "cache": {}, "trials": 0, "frozen": False}
 # (adding the library's own split for each tile, which fills whole rounds of the chip and won
 # several isolated trials, measured 36.22-36.26 vs 36.10-36.14 ms/step in round 3)
 _WG_SPLITS = (1, 2, 4, 8, 16, 32, 64)
@@ -416,7 +419,7 @@ def _tuned_data_split(lib, d, op, device, launch):
     if hit is not None:
         d.data_ksplit, d.data_algo = hit
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_current_stream_capturing() or AUTOTUNE["frozen"]:
         return (0, 0)
     times = {}
     torch.cuda.synchronize()
@@ -450,7 +453,7 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     hit = AUTOTUNE["cache"].get(key)
     if hit is not None:
         return hit
-    if not AUTOTUNE["enabled"] or d.dtype == TPG_F32:
+    if not AUTOTUNE["enabled"] or d.dtype == TPG_F32 or AUTOTUNE["frozen"]:
         return (0, 0)
     scratch = torch.empty_strided(dwv.shape, dwv.stride(), dtype=torch.float32, device=dwv.device)
     npix = d.n * (d.in_h * d.in_w if d.transposed else d.out_h * d.out_w)
@@ -837,7 +840,10 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
     # probing the weight gradient (bench.py roofline, tools/trace_step.py): the same two calls
     # as the side-stream split, both on this stream, events around the second -- the kernels
     # and their order on the stream are the fused call's (input gradient, then weight gradient)
-    probe_w = (not split and not grouped and dwt is not None and (dbias is None or fused_b) and
+    # (only where the split's own conditions hold -- dW and the bias into the flat buffers, no
+    # parked residual gradient: a local dw buffer would otherwise be dropped below)
+    probe_w = (not split and not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
+               ctx.link_res is None and
                not ctx.geom.transposed and PROBE["match"] is not None and PROBE["match"](d, "wgrad") and
                not torch.cuda.is_current_stream_capturing())
     if probe_w:
@@ -1422,7 +1428,10 @@ class _ImageLosses(torch.autograd.Function):
 def image_losses(x, target, w_pix, w_sym, w_tv):
     """w_pix * mean|x - target| + w_sym * mean|x - flip_W(x)| + w_tv * (mean |vertical| + mean
     |horizontal| neighbour differences of x), as one fp32 scalar (the G step's pixel,
-    symmetry and total-variation terms, tpgan_train._g_losses)."""
+    symmetry and total-variation terms, tpgan_train._g_losses).  Gradients flow to x only: a
+    target that requires grad is refused rather than silently left without one."""
+    if target.requires_grad and torch.is_grad_enabled():
+        raise ValueError("image_losses: the target must not require grad (no gradient is computed for it)")
     return _ImageLosses.apply(x, target, float(w_pix), float(w_sym), float(w_tv))
 
 
@@ -1471,6 +1480,8 @@ def l1_means(pairs, weights):
     from tpgan_lib import L1_MAX_SEGS
     if not 1 <= len(pairs) <= L1_MAX_SEGS or len(weights) != len(pairs):
         raise ValueError("l1_means: 1..%d pairs with one weight each" % L1_MAX_SEGS)
+    if torch.is_grad_enabled() and any(b.requires_grad for _, b in pairs):
+        raise ValueError("l1_means: the b_i must not require grad (gradients flow to the a_i only)")
     return _L1Set.apply(tuple(float(w) for w in weights), *[t for p in pairs for t in p])
 
 

@@ -484,6 +484,8 @@ class TPGANTrainer:
         self.gp = gradient_penalty
         self.gp_frozen_first_order = True  # (gradient_penalty: D frozen in the first-order pass; False = A/B)
         self._tuned_ungrouped = False
+        self._nsteps = 0
+        self.tune_steps = 3  # the tuning window (tpgan_ops.AUTOTUNE["frozen"] after it)
         self.sync = GradSync(process_group)
         self.world = self.sync.world
         # G's 551 MB of gradients are reduced bucket by bucket during the G backward, D's 54 MB
@@ -517,6 +519,8 @@ class TPGANTrainer:
         self.real_ahead_used = 0  # steps whose D(real) came from the previous step's real_ahead pass
         self._capturing = False
         self._segmented = False
+        self.comm_timing = False  # exposed-communication events around each exchange (exposed_comm_ms)
+        self.comm_events = []
         self.identity_fn = identity_fn
         self.sync.broadcast(self.fG)
         self.sync.broadcast(self.fD)
@@ -526,10 +530,46 @@ class TPGANTrainer:
 
     def _allreduce(self, flat):
         ov = self.gsync if flat is self.fG else self.dsync
+        # comm_timing (bench.py at world > 1): HIP events on the compute stream around the
+        # exchange -- the first is reached once the backward's kernels are enqueued ahead of it,
+        # the second once that stream has waited for the last bucket's all-reduce, so their
+        # distance is the communication time the compute stream was left waiting for
+        # (exposed), not the all-reduce time
+        t = self.comm_timing and flat.grad.is_cuda and self.world > 1
+        if t:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         if ov is not None and ov.active:
             ov.finish()
         else:
             self.sync.allreduce(flat)
+        if t:
+            e1.record()
+            self.comm_events.append(("G" if flat is self.fG else "D", e0, e1))
+
+    def exposed_comm_ms(self):
+        """{"G": ms, "D": ms, "steps": n} summed over the steps recorded since the last call
+        (comm_timing on); synchronises on the recorded events."""
+        out = {"G": 0.0, "D": 0.0}
+        for tag, e0, e1 in self.comm_events:
+            e1.synchronize()
+            out[tag] += e0.elapsed_time(e1)
+        n = sum(1 for tag, _, _ in self.comm_events if tag == "G")
+        self.comm_events = []
+        out["steps"] = n
+        return out
+
+    def bucket_stats(self):
+        """Gradient buckets of the data-parallel exchange: count and bytes per network."""
+        out = {}
+        for tag, ov, flat in (("G", self.gsync, self.fG), ("D", self.dsync, self.fD)):
+            if ov is None:
+                out[tag] = {"buckets": 1 if self.world > 1 else 0, "bytes": flat.grad.numel() * 4, "overlapped": False}
+            else:
+                sizes = [n * 4 for _, n in ov.spans]
+                out[tag] = {"buckets": len(sizes), "bytes": sum(sizes), "min_bucket_bytes": min(sizes),
+                            "max_bucket_bytes": max(sizes), "overlapped": True}
+        return out
 
     # The step is three device phases separated by the two data-parallel exchanges:
     #   A: zero grads, G forward, D-step forward/backward           -> all-reduce D grads
@@ -797,14 +837,23 @@ class TPGANTrainer:
                 return self.step(b, next_b)
             finally:
                 tpgan_ops.GROUP["enabled"] = prev
-        self._phase_a(b)
-        with tpgan_ops.roctx_range("allreduce-D"):
-            self._allreduce(self.fD)
-        self._phase_b(b)
-        self._real_ahead(next_b)
-        with tpgan_ops.roctx_range("allreduce-G"):
-            self._allreduce(self.fG)
-        return self._phase_c(b)
+        # the autotuners time new shapes during this trainer's first tune_steps steps only; a
+        # shape first seen later (a partial last batch) takes the planner's default plan rather
+        # than synchronising the device for a tuning sweep mid-training
+        frozen = tpgan_ops.AUTOTUNE["frozen"]
+        tpgan_ops.AUTOTUNE["frozen"] = frozen or self._nsteps >= self.tune_steps
+        self._nsteps += 1
+        try:
+            self._phase_a(b)
+            with tpgan_ops.roctx_range("allreduce-D"):
+                self._allreduce(self.fD)
+            self._phase_b(b)
+            self._real_ahead(next_b)
+            with tpgan_ops.roctx_range("allreduce-G"):
+                self._allreduce(self.fG)
+            return self._phase_c(b)
+        finally:
+            tpgan_ops.AUTOTUNE["frozen"] = frozen
 
     def capture(self, b, warmup=3, segmented=None):
         """Record the train step as hipGraphs (torch.cuda.CUDAGraph over HIP streams): one
@@ -839,20 +888,32 @@ class TPGANTrainer:
         self._segmented = bool(segmented)
         phases = (self._phase_a, self._phase_b, self._phase_c)
         self._graphs = []
-        if not segmented:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for ph in phases:
-                    out = ph(self._static)
-            self._graphs.append(g)
-        else:
-            pool = None
-            for ph in phases:
+        # no cyclic garbage collection while a graph is being recorded: a collection run inside
+        # the capture window (triggered by any allocation of Python objects) would free the
+        # device memory of whatever unreachable cycle it finds -- a dropped trainer, a stale
+        # autograd graph -- and a free during capture aborts the process.  The collect() above
+        # empties what exists now; this keeps anything that becomes garbage meanwhile alive
+        # until the capture has ended.
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            if not segmented:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    out = ph(self._static)
-                pool = g.pool()
+                with torch.cuda.graph(g):
+                    for ph in phases:
+                        out = ph(self._static)
                 self._graphs.append(g)
+            else:
+                pool = None
+                for ph in phases:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        out = ph(self._static)
+                    pool = g.pool()
+                    self._graphs.append(g)
+        finally:
+            if gc_was_enabled:
+                gc.enable()
         self._graph_out = out
         self._graph_layout = (self.fG.layout_version, self.fD.layout_version)
         torch.cuda.synchronize()
