@@ -103,6 +103,13 @@ typedef struct tpg_conv_desc {
                                      taps: 0 = planner's rule, 1 = the halo-tiled kernel, 2 = the
                                      tap-DMA pointwise kernel where eligible (16-bit, channels a
                                      multiple of 32); set by autotuners */
+  int32_t in_act;                 /* tpg_conv2d_bwd only: TPG_ACT_* of the layer that PRODUCED x (x = that
+                                     layer's activated output, saved by this op's forward): the input
+                                     gradient leaves the launch as dx * in_act'(x) -- the producer's
+                                     activation backward, applied in this launch's epilogue (after a
+                                     DX_ACCUM add), so the producer's own backward takes it as its
+                                     already-masked g.  0 (TPG_ACT_NONE) everywhere else */
+  float in_slope;                 /* LeakyReLU negative slope of in_act */
 } tpg_conv_desc;
 
 enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2, TPG_FLAG_DX_ACCUM = 4 };
@@ -156,7 +163,9 @@ int32_t tpg_conv2d_bwd_filter(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor g
  * gradient's halo is staged (the input-gradient launch writes g as it goes) and the bias sum
  * rides on the weight-gradient launch (one MFMA against ones per fragment); other layers run
  * tpg_act_bwd first.  w may be a pre-packed image (desc.flags WPACKED, bwd_data layout).
- * g must have y's strides for the fused form. */
+ * g must have y's strides for the fused form.  desc.in_act != NONE: dx = (input gradient
+ * [+ dx's DX_ACCUM entry values]) * in_act'(x), fused into the input-gradient epilogue where x
+ * has dx's strides (an in-place pass over dx otherwise); needs x and dx. */
 int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tensor w, tpg_tensor y, tpg_tensor gy,
                        tpg_tensor g, tpg_tensor dx, tpg_tensor dw, float* dbias, void* ws, size_t ws_bytes,
                        tpg_stream_t stream);

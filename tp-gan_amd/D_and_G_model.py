@@ -227,31 +227,33 @@ class GlobalPathway(nn.Module):
         deconv_64 = self.deconv_64(deconv_32)
         deconv_128 = self.deconv_128(deconv_64)
         add_conv_and_deconv_8 = self.add_conv_and_deconv_8(cat([deconv_8, conv4]))
-        enhance_features_8 = self.enhance_features_8(add_conv_and_deconv_8)
+        enhance_features_8 = self.enhance_features_8(add_conv_and_deconv_8, act_in_ok=True)
         assert enhance_features_8.shape[2] == self.img_size // 16  # :301
-        upsample_16 = self.upsample_16(enhance_features_8)
+        upsample_16 = self.upsample_16(enhance_features_8, act_in_ok=True)
         add_conv_and_deconv_16 = self.add_conv_and_deconv_16(conv3)
         enhance_features_16 = self.enhance_features_16(cat([upsample_16, add_conv_and_deconv_16]))
         assert enhance_features_16.shape[2] == self.img_size // 8  # :308
-        upsample_32 = self.upsample_32(enhance_features_16)
+        upsample_32 = self.upsample_32(enhance_features_16, act_in_ok=True)
         add_conv_and_deconv_32 = self.add_conv_and_deconv_32(cat([deconv_32, conv2]))
         enhance_features_32 = self.enhance_features_32(cat([upsample_32, add_conv_and_deconv_32]))
-        upsample_64 = self.upsample_64(enhance_features_32)
+        upsample_64 = self.upsample_64(enhance_features_32, act_in_ok=True)
         add_conv_and_deconv_64 = self.add_conv_and_deconv_64(cat([deconv_64, conv1]))
         enhance_features_64 = self.enhance_features_64(cat([upsample_64, add_conv_and_deconv_64]))
-        upsample_128 = self.upsample_128(enhance_features_64)
+        upsample_128 = self.upsample_128(enhance_features_64, act_in_ok=True)
         add_conv_and_deconv_128 = self.add_conv_and_deconv_128(cat([deconv_128, conv0, I128]))
         return upsample_128, add_conv_and_deconv_128, fc2
 
     def decode_128(self, enc, local_fake_image, local_feature):
-        """The 128-px fusion with the local features (:321-329)."""
+        """The 128-px fusion with the local features (:321-329).  (act_in_ok: each of these
+        outputs feeds the next module alone, so its consumer applies its activation backward,
+        tpgan_ops.ActToken; likewise in encode() for the decoder's enhance -> upsample chain.)"""
         cat = tpgan_ops.cat
         upsample_128, add_conv_and_deconv_128, fc2 = enc
         enhance_features_128 = self.enhance_features_128(
             cat([upsample_128, add_conv_and_deconv_128, local_feature, local_fake_image]))
-        conv5 = self.conv5(enhance_features_128)
-        conv6 = self.conv6(conv5)
-        decoded_img128 = self.decoded_img128(conv6)
+        conv5 = self.conv5(enhance_features_128, act_in_ok=True)
+        conv6 = self.conv6(conv5, act_in_ok=True)
+        decoded_img128 = self.decoded_img128(conv6, act_in_ok=True)
         return decoded_img128, fc2
 
 

@@ -71,7 +71,9 @@ class _FusedSequential(nn.Sequential):
             return pad, mods[0], (mods[1] if len(mods) == 2 else None)
         return None
 
-    def forward(self, x, residual=None, res_scale=1.0, post_act=None, link_res=None, link_dx=None):
+    def forward(self, x, residual=None, res_scale=1.0, post_act=None, link_res=None, link_dx=None, act_in_ok=False):
+        """act_in_ok: the caller's promise that x is consumed by this module alone, so the
+        first conv may apply x's producer activation backward (tpgan_ops.ActToken)."""
         parts = self._parts()
         if parts is not None:
             pad, layer, act = parts
@@ -79,10 +81,10 @@ class _FusedSequential(nn.Sequential):
                 if act is not None:
                     raise RuntimeError("residual fusion expects a conv without activation")
                 act = post_act
-            return _apply_conv(layer, x, pad, act, residual, res_scale, link_res, link_dx)
+            return _apply_conv(layer, x, pad, act, residual, res_scale, link_res, link_dx, act_in_ok)
         if residual is not None:
             raise RuntimeError("residual fusion needs a [pad] conv [act] sequence")
-        return _generic_forward(self, x)
+        return _generic_forward(self, x, act_in_ok)
 
 
 def _conv_geom_args(layer, pad_mod):
@@ -104,7 +106,7 @@ def _conv_geom_args(layer, pad_mod):
     return dict(stride=stride, pad=(ph, ph, pw, pw), pad_mode=PAD_ZERO)
 
 
-def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None):
+def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None, act_in_ok=False):
     if tuple(layer.dilation) != (1, 1) or layer.groups != 1:
         raise NotImplementedError("dilated / grouped convolution")
     if (isinstance(layer, nn.Conv2d) and layer.in_channels <= 4 and residual is None and link_dx is None and
@@ -115,10 +117,10 @@ def _apply_conv(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=N
         if y is not None:
             return y
     return tpgan_ops.conv2d(x, layer.weight, layer.bias, act=act, residual=residual, res_scale=res_scale,
-                            link_res=link_res, link_dx=link_dx, **_conv_geom_args(layer, pad_mod))
+                            link_res=link_res, link_dx=link_dx, act_in_ok=act_in_ok, **_conv_geom_args(layer, pad_mod))
 
 
-def _conv_call(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None):
+def _conv_call(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=None, link_dx=None, act_in_ok=False):
     """tpgan_ops.conv2d keyword arguments of _apply_conv's call, or None where it would not
     call conv2d (dilated / grouped convs)."""
     if tuple(layer.dilation) != (1, 1) or layer.groups != 1:
@@ -131,33 +133,36 @@ def _conv_call(layer, x, pad_mod, act, residual=None, res_scale=1.0, link_res=No
             a.update(bias=layer.bias, act=act)
             return a
     return dict(x=x, weight=layer.weight, bias=layer.bias, act=act, residual=residual, res_scale=res_scale,
-                link_res=link_res, link_dx=link_dx, **_conv_geom_args(layer, pad_mod))
+                link_res=link_res, link_dx=link_dx, act_in_ok=act_in_ok, **_conv_geom_args(layer, pad_mod))
 
 
-def group_forward(mods, xs):
+def group_forward(mods, xs, act_in_ok=False):
     """mods[k](xs[k]) for same-structured modules (the four LocalPathways' copies of one
     layer), in lockstep: each fused conv of the structure runs as ONE grouped node over all k
     (tpgan_ops.conv2d_group: one launch per kernel position instead of one per module).
-    Structures it does not know run module by module."""
+    Structures it does not know run module by module.  act_in_ok as in
+    _FusedSequential.forward (the same promise for every member)."""
     m0 = mods[0]
     if all(isinstance(m, _FusedSequential) for m in mods):
         parts = [m._parts() for m in mods]
         if all(p is not None for p in parts):
-            return _group_fused(mods, xs)
+            return _group_fused(mods, xs, act_in_ok=act_in_ok)
         kids = [list(m._modules.values()) for m in mods]
         if (all(p is None for p in parts) and all(len(k) == len(kids[0]) for k in kids) and
                 all(isinstance(c, (_FusedSequential, ResidualBlock)) for c in kids[0])):
             for i in range(len(kids[0])):
-                xs = group_forward([k[i] for k in kids], xs)
+                xs = group_forward([k[i] for k in kids], xs, act_in_ok=act_in_ok if i == 0 else True)
             return xs
     elif all(isinstance(m, ResidualBlock) for m in mods) and all(type(m) is type(m0) for m in mods):
-        out = _group_resblock(mods, xs)
+        out = _group_resblock(mods, xs, act_in_ok)
         if out is not None:
             return out
-    return [m(x) for m, x in zip(mods, xs)]
+    return [m(x, act_in_ok=act_in_ok) if isinstance(m, (_FusedSequential, ResidualBlock)) else m(x)
+            for m, x in zip(mods, xs)]
 
 
-def _group_fused(seqs, xs, residuals=None, res_scales=None, post_acts=None, links_res=None, links_dx=None):
+def _group_fused(seqs, xs, residuals=None, res_scales=None, post_acts=None, links_res=None, links_dx=None,
+                 act_in_ok=False):
     n = len(seqs)
     calls = []
     for k, (seq, x) in enumerate(zip(seqs, xs)):
@@ -168,19 +173,21 @@ def _group_fused(seqs, xs, residuals=None, res_scales=None, post_acts=None, link
                 raise RuntimeError("residual fusion expects a conv without activation")
             act = post_acts[k]
         c = _conv_call(layer, x, pad, act, residual, res_scales[k] if res_scales is not None else 1.0,
-                       links_res[k] if links_res is not None else None, links_dx[k] if links_dx is not None else None)
+                       links_res[k] if links_res is not None else None, links_dx[k] if links_dx is not None else None,
+                       act_in_ok)
         if c is None:
             return [seq(x, residual=(residuals[k] if residuals is not None else None),
                         res_scale=(res_scales[k] if res_scales is not None else 1.0),
                         post_act=(post_acts[k] if post_acts is not None else None),
                         link_res=(links_res[k] if links_res is not None else None),
-                        link_dx=(links_dx[k] if links_dx is not None else None)) for k, (seq, x) in enumerate(zip(seqs, xs))]
+                        link_dx=(links_dx[k] if links_dx is not None else None), act_in_ok=act_in_ok)
+                    for k, (seq, x) in enumerate(zip(seqs, xs))]
         calls.append(c)
     assert len(calls) == n
     return tpgan_ops.conv2d_group(calls)
 
 
-def _group_resblock(blocks, xs):
+def _group_resblock(blocks, xs, act_in_ok=False):
     """ResidualBlock.forward over the group; None where the block is not the fused form."""
     b0 = blocks[0]
     layers = [list(b.layers) for b in blocks]
@@ -193,9 +200,10 @@ def _group_resblock(blocks, xs):
         links = [tpgan_ops.GradLink() for _ in blocks]
     h = xs
     for i in range(len(layers[0]) - 1):
-        h = _group_fused([l[i] for l in layers], h, links_dx=links if i == 0 else None)
+        h = _group_fused([l[i] for l in layers], h, links_dx=links if i == 0 else None,
+                         act_in_ok=(act_in_ok and links is not None) if i == 0 else True)
     return _group_fused([l[-1] for l in layers], h, residuals=xs, res_scales=[b.scaling_factor for b in blocks],
-                        post_acts=[b.activation for b in blocks], links_res=links)
+                        post_acts=[b.activation for b in blocks], links_res=links, act_in_ok=True)
 
 
 def _link_ok(seq):
@@ -207,12 +215,20 @@ def _link_ok(seq):
     return layer.padding_mode == "zeros" and layer.kernel_size[0] * layer.kernel_size[1] <= 49
 
 
-def _generic_forward(seq, x):
+def _generic_forward(seq, x, act_in_ok=False):
     mods = list(seq._modules.values())
     i = 0
     pad = None
+    # a chain of fused modules: each one's output is consumed by the next alone (ActToken)
+    chain_ok = act_in_ok
     while i < len(mods):
         m = mods[i]
+        if isinstance(m, (_FusedSequential, ResidualBlock)):
+            x = m(x, act_in_ok=chain_ok)
+            chain_ok = True
+            i += 1
+            continue
+        chain_ok = False
         if isinstance(m, nn.ReflectionPad2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.Conv2d):
             pad = m
             i += 1
@@ -358,7 +374,8 @@ class ResidualBlock(nn.Module):
                               False))
         self.layers = nn.Sequential(*convs)
 
-    def forward(self, x):
+    def forward(self, x, act_in_ok=False):
+        """act_in_ok: x is consumed by this block alone (see _FusedSequential.forward)."""
         short = self.shortcut(x) if len(self.shortcut._modules) else x
         h = x
         layers = list(self.layers)
@@ -368,10 +385,16 @@ class ResidualBlock(nn.Module):
         # gradient launch instead of by autograd (tpgan_ops.GradLink)
         link = (tpgan_ops.GradLink() if tpgan_ops.RES_LINK["enabled"] and fused_last and short is x and len(layers) >= 2 and _link_ok(layers[0])
                 and torch.is_grad_enabled() else None)
+        # ActToken: the first conv sees the whole gradient of x only when the link carries the
+        # shortcut's part into its launch; the inner convs' inputs are this block's own
         for i, m in enumerate(layers[:-1]):
-            h = m(h, link_dx=link) if (i == 0 and link is not None) else m(h)
+            if i == 0:
+                h = m(h, link_dx=link, act_in_ok=act_in_ok and link is not None) if link is not None else m(h)
+            else:
+                h = m(h, act_in_ok=True)
         if fused_last:
-            return last(h, residual=short, res_scale=self.scaling_factor, post_act=self.activation, link_res=link)
+            return last(h, residual=short, res_scale=self.scaling_factor, post_act=self.activation, link_res=link,
+                        act_in_ok=len(layers) >= 2)
         lm = list(last._modules.values())
         if (tpgan_ops.act_code(self.activation) is not None and len(lm) == 2 and isinstance(lm[0], nn.Conv2d) and
                 isinstance(lm[1], nn.BatchNorm2d) and not lm[1].training):

@@ -784,10 +784,20 @@ struct HaloMask {
   float slope;
 };
 
+// desc.in_act: the input gradient's epilogue multiplies by act'(X) (X = the conv's input x, the
+// producer's activated output, read at the output's offsets); `applied` reports whether the
+// launched plan did (every problem on the halo / pointwise kernels, X laid out like Y)
+struct HaloXA {
+  tpg_tensor X;
+  int act;
+  float slope;
+  bool applied;
+};
+
 static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, const tpg_tensor& W, const float* bias,
                          int bias_mod, const tpg_tensor& R, float res_scale, const tpg_tensor& Y, int act, float slope,
                          char* ws, size_t ws_bytes, hipStream_t s, const char* packed = nullptr,
-                         const HaloMask* mk = nullptr) {
+                         const HaloMask* mk = nullptr, HaloXA* xa = nullptr) {
   size_t need = probs_ws(v);
   if (need > ws_bytes) return fail(-20, "workspace too small: %zu < %zu", ws_bytes, need);
   const bool vA = vec_ok(A, dtype);
@@ -811,6 +821,19 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
       P.halo = false;
       P.wp_bytes = P.g_wp;
       P.sk_bytes = P.g_sk;
+    }
+  }
+  // the producer's act' in the epilogues: all or nothing (a partial application could not be
+  // completed by the caller's separate pass without applying it twice)
+  const void* XA = nullptr;
+  if (xa) {
+    xa->applied = false;
+    bool ok = xa->X.data && xa->X.dtype == Y.dtype && xa->X.stride[0] == Y.stride[0] && xa->X.stride[2] == Y.stride[2] &&
+              xa->X.stride[3] == Y.stride[3] && xa->X.stride[1] == 1 && vec_ok(xa->X, dtype) == vec_ok(Y, dtype);
+    for (const Prob& P : v) ok = ok && P.halo;
+    if (ok) {
+      XA = xa->X.data;
+      xa->applied = true;
     }
   }
   size_t off = 0;
@@ -849,6 +872,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
         h.M = mk->M.data; h.m_sn = mk->M.stride[0]; h.m_sh = mk->M.stride[2]; h.m_sw = mk->M.stride[3];
         h.G = mk->G.data; h.mact = mk->act; h.mslope = mk->slope;
       }
+      h.XA = XA; h.xa_act = XA ? xa->act : 0; h.xa_slope = XA ? xa->slope : 0.f;
       int e = do_halo(h, dtype, P.hcfg, s, mk != nullptr);
       if (e) return hip_check(e, "halo conv");
       if (h.ksplit > 1) {
@@ -861,6 +885,7 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
         ep.bias = bias; ep.bias_mod = 0;
         ep.R = R.data; ep.r_sn = R.stride[0]; ep.r_sh = R.stride[2]; ep.r_sw = R.stride[3];
         ep.res_scale = res_scale; ep.act = act; ep.slope = slope; ep.dtype = dtype;
+        ep.XA = XA; ep.xa_act = XA ? xa->act : 0; ep.xa_slope = XA ? xa->slope : 0.f;
         e = do_epilogue(ep, s);
         if (e) return hip_check(e, "halo epilogue");
       }
@@ -1004,11 +1029,21 @@ extern "C" int32_t tpg_conv2d_fwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
                    packed ? reinterpret_cast<const char*>(w.data) : nullptr);
 }
 
+static int32_t bwd_data_impl(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx, void* ws,
+                             size_t ws_bytes, tpg_stream_t stream, HaloXA* xa);
+
 extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx, void* ws,
                                        size_t ws_bytes, tpg_stream_t stream) {
   ShareScope share_scope(d);
   int32_t rc = check_desc(d);
   if (rc) return rc;
+  if (d->in_act != TPG_ACT_NONE) return fail(-33, "bwd_data: desc.in_act needs x (tpg_conv2d_bwd)");
+  return bwd_data_impl(d, g, w, dx, ws, ws_bytes, stream, nullptr);
+}
+
+static int32_t bwd_data_impl(const tpg_conv_desc* d, tpg_tensor g, tpg_tensor w, tpg_tensor dx, void* ws,
+                             size_t ws_bytes, tpg_stream_t stream, HaloXA* xa) {
+  int32_t rc;
   if ((rc = check_tensor(g, d->dtype, "g")) || (rc = check_tensor(dx, d->dtype, "dx"))) return rc;
   const bool packed = d->flags & TPG_FLAG_WPACKED;
   if (!w.data || (w.dtype != TPG_F32 && !packed)) return fail(-13, "weight must be fp32");
@@ -1028,7 +1063,7 @@ extern "C" int32_t tpg_conv2d_bwd_data(const tpg_conv_desc* d, tpg_tensor g, tpg
   if (acc && (comp || refl)) return fail(-32, "dx accumulation: zero-padded, non-GEMM-form geometries only");
   if (!refl)
     return run_probs(v, d->dtype, g, w, nullptr, 0, acc ? dx : none, acc ? 1.f : 0.f, dx, TPG_ACT_NONE, 0.f,
-                     reinterpret_cast<char*>(ws), ws_bytes, s, pk);
+                     reinterpret_cast<char*>(ws), ws_bytes, s, pk, nullptr, xa);
   // reflect: gradient of the padded input into a dense NHWC temp, then fold onto dx
   const size_t tmpb = reflect_tmp_bytes(d);
   if (ws_bytes < tmpb) return fail(-20, "workspace too small");
@@ -1290,6 +1325,15 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   const tpg_tensor& G = g_is_gy ? gy : g;
   bool have_g = g_is_gy, bias_done = false, dx_done = false;
   const bool acc = dx.data && (d->flags & TPG_FLAG_DX_ACCUM);
+  // desc.in_act: dx leaves as dx * in_act'(x) (the producer's activation backward)
+  HaloXA xa;
+  memset(&xa, 0, sizeof(xa));
+  const bool xact = dx.data && d->in_act != TPG_ACT_NONE;
+  if (xact) {
+    if (d->in_act < TPG_ACT_NONE || d->in_act > TPG_ACT_RELU6) return fail(-2, "conv2d_bwd: bad in_act %d", d->in_act);
+    if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(dx, d->dtype, "dx"))) return rc;
+    xa.X = x; xa.act = d->in_act; xa.slope = d->in_slope;
+  }
   if (acc && (bwd_data_composite(d, nullptr, nullptr) || (!d->transposed && d->pad_mode == TPG_PAD_REFLECT)))
     return fail(-32, "dx accumulation: zero-padded, non-GEMM-form geometries only");
   // pre-packed weights that the input-gradient plan of these tensors cannot use: report it
@@ -1314,7 +1358,7 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
       memset(&none, 0, sizeof(none));
       rc = run_probs(v, d->dtype, gy, w, nullptr, 0, acc ? dx : none, acc ? 1.f : 0.f, dx, TPG_ACT_NONE, 0.f,
                      reinterpret_cast<char*>(ws), ws_bytes, s, packed ? reinterpret_cast<const char*>(w.data) : nullptr,
-                     &mk);
+                     &mk, xact ? &xa : nullptr);
       if (rc == 0) have_g = dx_done = true;
       else if (rc != -31) return rc;
     }
@@ -1333,7 +1377,13 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
     bias_done = db != nullptr;
   }
   if (dx.data && !dx_done) {
-    if ((rc = tpg_conv2d_bwd_data(d, G, w, dx, ws, ws_bytes, stream))) return rc;
+    xa.applied = false;
+    if ((rc = bwd_data_impl(d, G, w, dx, ws, ws_bytes, stream, xact ? &xa : nullptr))) return rc;
+  }
+  if (xact && !xa.applied) {  // (plans whose epilogue cannot take it: one in-place pass over dx)
+    rc = hip_check(do_act_bwd(d->n, d->in_c, d->in_h, d->in_w, d->in_act, d->in_slope, dx, x, dx, nullptr, s),
+                   "act_bwd (in_act)");
+    if (rc) return rc;
   }
   // 3. the weight gradient, summing the bias gradient in the same launch where it can
   if (dw.data) {

@@ -453,6 +453,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   float* s_acc = reinterpret_cast<float*>(lds) + BM * 4 + 256;  // [RP][LDW]
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
+  const E* XA = reinterpret_cast<const E*>(p.XA);
   float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
   for (int q = tid; q < BM; q += 512) {
     const int sub = q / THW, rem = q - sub * THW;
@@ -518,7 +519,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       // residual vectors of every group first (all loads in flight), then finish and store
       // (bf16; the fp32 parity mode loads them in the finishing loop: register budget)
       constexpr int PF = BF ? IPT : 0;
-      u32x4 rv[IPT][NV];
+      u32x4 rv[IPT][NV], xv[IPT][NV];
 #pragma unroll
       for (int k = 0; k < (R ? PF : 0); ++k) {
         const int it = min(tid + 512 * k, RP * CG - 1);  // clamped past the last group
@@ -528,6 +529,17 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         const u32x4* src = reinterpret_cast<const u32x4*>(R + (ok ? s_off[2 * (pass * RP + row) + 1] + n0 + c0 : 0));
 #pragma unroll
         for (int v = 0; v < NV; ++v) rv[k][v] = src[v];
+      }
+      // desc.in_act: the producer's activation input x at the output's offsets (yvec: X has Y's
+      // strides and alignment), prefetched the same way
+#pragma unroll
+      for (int k = 0; k < (XA ? PF : 0); ++k) {
+        const int it = min(tid + 512 * k, RP * CG - 1);
+        const int row = it / CG, c0 = (it - row * CG) * 8;
+        const bool ok = p.yvec && p.Nout - (n0 + c0) >= 8 && s_off[2 * (pass * RP + row)] >= 0;
+        const u32x4* src = reinterpret_cast<const u32x4*>(XA + (ok ? s_off[2 * (pass * RP + row)] + n0 + c0 : 0));
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xv[k][v] = src[v];
       }
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
@@ -561,8 +573,21 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
           for (int e = 0; e < 8; ++e) v[e] += p.res_scale * (float)rr.e[e];
         }
         union { u32x4 u[NV]; E e[8]; } o;
+        if (XA) {  // input gradient for the producer: v * xa_act'(x)
+          union { u32x4 u[NV]; E e[8]; } xx;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o.e[e] = (E)h_act(v[e], p.act, p.slope);
+          for (int q = 0; q < NV; ++q) xx.u[q] = xv[k][q];
+          if (!(full && p.yvec && BF)) {
+            const E* xs = XA + yo + col0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xx.e[e] = e < ncol ? xs[e] : (E)0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.e[e] = (E)h_act(v[e], p.act, p.slope);
+        }
         E* dst = Y + yo + col0;
         if (full && p.yvec) {
 #pragma unroll

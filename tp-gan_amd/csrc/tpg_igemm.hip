@@ -277,6 +277,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
   const int JHJW = p.JH * p.JW;
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
+  const E* XA = reinterpret_cast<const E*>(p.XA);  // (desc.in_act: Y's offsets)
   const bool small = (int64_t)p.M * p.Nout < (1ll << 31);  // 32-bit index math (uniform)
   for (int64_t idx = b0 * blockDim.x + threadIdx.x; idx < total; idx += nb * blockDim.x) {
     const int64_t e0 = idx * V;
@@ -313,13 +314,15 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
       // the parked round-3 version of this path read the first residual four times)
       // (the base pointers too: a channel-offset view through the public C API may start on
       // any 2-byte boundary)
-      if (((yo | (R ? ro : 0)) & 3) == 0 && (((uintptr_t)Y | (uintptr_t)R) & 7) == 0) {
-        uint2 rw = make_uint2(0u, 0u);
+      if (((yo | (R ? ro : 0)) & 3) == 0 && (((uintptr_t)Y | (uintptr_t)R | (uintptr_t)XA) & 7) == 0) {
+        uint2 rw = make_uint2(0u, 0u), xw = make_uint2(0u, 0u);
         if (R) rw = *reinterpret_cast<const uint2*>(R + ro);
+        if (XA) xw = *reinterpret_cast<const uint2*>(XA + yo);
         uint32_t ow[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t w = h ? rw.y : rw.x;
+          const uint32_t xh = h ? xw.y : xw.x;
           uint32_t packed = 0;
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
@@ -330,7 +333,13 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
               const unsigned short r16 = (unsigned short)(e ? (w >> 16) : (w & 0xffffu));
               x += p.res_scale * (float)__builtin_bit_cast(E, r16);
             }
-            const E o = (E)act_apply(x, p.act, p.slope);
+            E o;
+            if (XA) {
+              const unsigned short x16 = (unsigned short)(e ? (xh >> 16) : (xh & 0xffffu));
+              o = (E)tpg_act_grad(x, (float)__builtin_bit_cast(E, x16), p.xa_act, p.xa_slope);
+            } else {
+              o = (E)act_apply(x, p.act, p.slope);
+            }
             const unsigned short o16 = __builtin_bit_cast(unsigned short, o);
             packed |= (uint32_t)o16 << (16 * e);
           }
@@ -345,7 +354,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
       float x = v[u];
       if (p.bias) x += p.bias[p.bias_mod ? (col + u) % p.bias_mod : col + u];
       if (R) x += p.res_scale * ld_f(R + ro + u);
-      st_f(Y + yo + u, act_apply(x, p.act, p.slope));
+      st_f(Y + yo + u, XA ? tpg_act_grad(x, ld_f(XA + yo + u), p.xa_act, p.xa_slope) : act_apply(x, p.act, p.slope));
     }
   }
 }

@@ -350,6 +350,10 @@ struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [
   int act;
   float slope;
   int dtype;
+  // input-gradient epilogues (desc.in_act): Y = v * xa_act'(XA), XA read at Y's offsets
+  const void* XA;
+  int xa_act;
+  float xa_slope;
 };
 
 // ---------------------------------------------------------------- halo direct conv ----
@@ -393,6 +397,11 @@ struct HaloArgs {
   void* G;
   int mact;
   float mslope;
+  // input-gradient epilogue (desc.in_act: the producer of the conv's input x applied act'):
+  // the output is v * xa_act'(XA) instead of act(v); XA (= x) is read at Y's element offsets
+  const void* XA;
+  int xa_act;
+  float xa_slope;
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 

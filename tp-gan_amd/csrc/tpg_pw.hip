@@ -229,6 +229,7 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
   __syncthreads();
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
+  const E* XA = reinterpret_cast<const E*>(p.XA);
   for (int it = tid; it < BM * CG; it += 256) {
     const int row = it / CG, c0 = (it - row * CG) * 8;
     const int64_t yo = s_off[2 * row];
@@ -267,8 +268,22 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
       for (int e = 0; e < 8; ++e) v[e] += p.res_scale * (float)rr.e[e];
     }
     union { u32x4 u[NV]; E e[8]; } o;
+    if (XA) {  // desc.in_act: v * xa_act'(x), x at the output's offsets
+      union { u32x4 u[NV]; E e[8]; } xx;
+      const E* xs = XA + yo + col0;
+      if (full && p.yvec) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act(v[e], p.act, p.slope);
+        for (int q = 0; q < NV; ++q) xx.u[q] = reinterpret_cast<const u32x4*>(xs)[q];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xx.e[e] = e < ncol ? xs[e] : (E)0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act(v[e], p.act, p.slope);
+    }
     E* dst = Y + yo + col0;
     if (full && p.yvec) {
 #pragma unroll

@@ -34,7 +34,7 @@ class ConvDesc(ctypes.Structure):
         "pad_t", "pad_b", "pad_l", "pad_r", "pad_mode", "transposed", "dtype", "act")] + [
         ("slope", ctypes.c_float), ("res_scale", ctypes.c_float), ("ksplit", ctypes.c_int32),
         ("algo", ctypes.c_int32), ("flags", ctypes.c_int32), ("data_ksplit", ctypes.c_int32),
-        ("data_algo", ctypes.c_int32)]
+        ("data_algo", ctypes.c_int32), ("in_act", ctypes.c_int32), ("in_slope", ctypes.c_float)]
 
 
 class L1Seg(ctypes.Structure):  # tpg_l1_seg

@@ -14,6 +14,7 @@ Master weights and their gradients stay float32.
 import contextlib
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -594,7 +595,7 @@ def _ws(lib, desc, op, device):
 
 
 def _conv_act_forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res=None, link_dx=None,
-                      keep=None):
+                      keep=None, links=None):
     """_ConvAct's forward on any ctx with save_for_backward (a _MemberCtx inside a grouped
     node); keep: a list that holds every temporary a deferred (grouped) launch still reads."""
     lib = load()
@@ -651,6 +652,7 @@ def _conv_act_forward(ctx, x, weight, bias, residual, geom, act, slope, res_scal
     ctx.res_dtype = residual.dtype if residual is not None else None
     ctx.x_dtype = x.dtype
     ctx.link_res, ctx.link_dx = link_res, link_dx
+    ctx.act_in, ctx.act_out = links if links is not None else (None, None)
     return y
 
 
@@ -660,17 +662,20 @@ class _ConvAct(torch.autograd.Function):
     saved input and output, never the pre-activation)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res=None, link_dx=None):
+    def forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res=None, link_dx=None,
+                links=None):
         return _conv_act_forward(ctx, x, weight, bias, residual, geom, act, slope, res_scale, wparam, link_res,
-                                 link_dx)
+                                 link_dx, links=links)
 
     @staticmethod
     def backward(ctx, gy):
         if torch.is_grad_enabled():  # create_graph=True (WGAN-GP): differentiable backward
-            return tuple(_conv_act_backward_graph(ctx, gy)) + (None, None)
+            _act_out_taken(ctx, gy, allowed=False)
+            return tuple(_conv_act_backward_graph(ctx, gy)) + (None, None, None)
         if FUSED_BWD["enabled"]:
-            return _conv_act_backward_fused(ctx, gy) + (None, None)
-        return _ConvAct._backward_three_calls(ctx, gy) + (None, None)
+            return _conv_act_backward_fused(ctx, gy) + (None, None, None)
+        _act_out_taken(ctx, gy, allowed=False)
+        return _ConvAct._backward_three_calls(ctx, gy) + (None, None, None)
 
     @staticmethod
     def _backward_three_calls(ctx, gy):
@@ -761,8 +766,11 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
     need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
     need_db = ctx.has_bias and ctx.needs_input_grad[2]
     gy = _fix_c1(gy)
+    # ActToken (producer side): the consumer's input-gradient launch already applied this conv's
+    # act', so gy IS g -- the backward runs as that of the un-activated conv
+    act_eff = ACT_NONE if _act_out_taken(ctx, gy) else ctx.act
     es = 4 if dtype == torch.float32 else 2
-    g_is_gy = (ctx.act == ACT_NONE and gy.dtype == dtype and gy.dim() == 4 and gy.stride(1) == 1 and
+    g_is_gy = (act_eff == ACT_NONE and gy.dtype == dtype and gy.dim() == 4 and gy.stride(1) == 1 and
                gy.data_ptr() % 16 == 0 and all((gy.stride(i) * es) % 16 == 0 for i in (0, 2, 3)))
     g = gy if g_is_gy else _fix_c1(new_act(n, cout, oh, ow, dtype, y.device))
     dbias = None
@@ -780,6 +788,29 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
         d.flags = d.flags | FLAG_DX_ACCUM
     else:
         dx = new_act(*x.shape, dtype=dtype, device=x.device) if need_dx else None
+    # ActToken (consumer side): x is the activated output of a conv whose only gradient is this
+    # launch's dx (+ the parked shortcut gradient, when the residual block's link carried it in):
+    # the launch leaves dx * act_x'(x) for that producer (desc.in_act)
+    tok_in = ctx.act_in
+    fuse_in = (tok_in is not None and ACT_LINK["enabled"] and need_dx and acc is None and
+               (ctx.link_dx is None or bool(d.flags & FLAG_DX_ACCUM)))
+    d.act = act_eff
+    if fuse_in:
+        d.in_act, d.in_slope = tok_in.act, tok_in.slope
+    try:
+        out = _conv_act_backward_fused_body(ctx, gy, keep, lib, x, weight, y, d, dtype, n, cout, oh, ow, need_dx, need_dw,
+                                            g_is_gy, g, dbias, fused_b, acc, dx, act_eff)
+    finally:
+        d.act = ctx.act
+        d.in_act, d.in_slope = ACT_NONE, 0.0
+    if fuse_in and out[0] is not None:
+        tok_in.pre = out[0]
+    return out
+
+
+def _conv_act_backward_fused_body(ctx, gy, keep, lib, x, weight, y, d, dtype, n, cout, oh, ow, need_dx, need_dw,
+                                  g_is_gy, g, dbias, fused_b, acc, dx, act_eff):
+    grouped = keep is not None
     dw = dwv = None
     if need_dw:
         tgt = _fused_target(ctx.wparam)
@@ -840,10 +871,10 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
     # probing the weight gradient (bench.py roofline, tools/trace_step.py): the same two calls
     # as the side-stream split, both on this stream, events around the second -- the kernels
     # and their order on the stream are the fused call's (input gradient, then weight gradient)
-    # (only where the split's own conditions hold -- dW and the bias into the flat buffers, no
-    # parked residual gradient: a local dw buffer would otherwise be dropped below)
+    # (only where dW and the bias go into the flat buffers: a local dw buffer would otherwise be
+    # dropped below.  A parked residual gradient is fine here: both calls stay on this stream,
+    # ahead of the first conv's in-place write of it)
     probe_w = (not split and not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
-               ctx.link_res is None and
                not ctx.geom.transposed and PROBE["match"] is not None and PROBE["match"](d, "wgrad") and
                not torch.cuda.is_current_stream_capturing())
     if probe_w:
@@ -912,7 +943,10 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
     dres = None
     if ctx.has_res and ctx.needs_input_grad[3]:
         dres = g if ctx.res_scale == 1.0 else g * ctx.res_scale
-        if ctx.link_res is not None and dres is not gy and dres.dtype == dtype:
+        # (gy itself only when it is the ActToken consumer's input gradient: then this backward
+        # owns it, and the first conv may accumulate into it in place)
+        if ctx.link_res is not None and (dres is not gy or act_eff == ACT_NONE and ctx.act != ACT_NONE) and \
+                dres.dtype == dtype:
             # park it for the block's first conv (its input-gradient launch adds it)
             ctx.link_res.g = dres
             dres = None
@@ -937,6 +971,7 @@ def _plain_desc(d):
     e = ConvDesc()
     ctypes.memmove(ctypes.byref(e), ctypes.byref(d), ctypes.sizeof(ConvDesc))
     e.act, e.slope, e.res_scale, e.ksplit, e.algo, e.data_ksplit, e.data_algo = ACT_NONE, 0.0, 1.0, 0, 0, 0, 0
+    e.in_act, e.in_slope = ACT_NONE, 0.0
     return e
 
 
@@ -1096,17 +1131,94 @@ def _fused_target(p):
 
 
 def conv2d(x, weight, bias=None, stride=(1, 1), pad=(0, 0, 0, 0), pad_mode=PAD_ZERO, act=None, residual=None,
-           res_scale=1.0, transposed=False, output_padding=(0, 0), wparam=None, link_res=None, link_dx=None):
+           res_scale=1.0, transposed=False, output_padding=(0, 0), wparam=None, link_res=None, link_dx=None,
+           act_in_ok=False):
     """Functional entry: act is an activation module (LeakyReLU / ReLU) or None.  link_res /
     link_dx: a GradLink shared by a residual block's last conv (residual = the block input)
-    and its first conv (input = the block input), see GradLink."""
+    and its first conv (input = the block input), see GradLink.  act_in_ok: the caller's
+    promise that x is consumed by this conv alone (with link_dx: and by the shortcut whose
+    gradient the link carries into this conv's input gradient) -- see ActToken."""
     code = act_code(act)
     if code is None:
         raise ValueError("activation %r cannot be fused" % (act,))
     kh, kw = weight.shape[2], weight.shape[3]
     geom = ConvGeom(kh, kw, stride, pad, pad_mode, transposed, output_padding)
-    return _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale), wparam, link_res,
-                          link_dx)
+    links = _act_links(x, code, act_in_ok)
+    y = _ConvAct.apply(x, weight, bias, residual, geom, code[0], code[1], float(res_scale), wparam, link_res,
+                       link_dx, links)
+    _set_act_token(links, y)
+    return y
+
+
+def _act_links(x, code, act_in_ok):
+    """(token of x to apply in this conv's input gradient, token of this conv's output), or None."""
+    if not (ACT_LINK["enabled"] and torch.is_grad_enabled()):
+        return None
+    tok_in = getattr(x, "_tpg_act_tok", None) if act_in_ok else None
+    if tok_in is not None and (tok_in.y is None or tok_in.y() is not x or x.dtype != get_compute_dtype()):
+        tok_in = None  # (converted on the way in: the gradient would pass through the conversion)
+    tok_out = ActToken(code[0], code[1]) if code[0] != ACT_NONE else None
+    return (tok_in, tok_out)
+
+
+def _set_act_token(links, y):
+    if links is not None and links[1] is not None:
+        links[1].y = weakref.ref(y)
+        y._tpg_act_tok = links[1]
+
+
+class ActToken(object):
+    """The producer's activation backward, moved into its consumer's input-gradient launch.
+
+    A fused conv with an activation (ModificationLayer.py:54-123 conv(): Conv2d + LeakyReLU /
+    ReLU) saves its output y; its backward would stage g = gy * act'(y) -- reading y a second
+    time as a halo beside gy (the masked input gradient) or in a separate activation-backward
+    pass.  When y is consumed by ONE conv alone (a residual block's inner conv pair, a chain of
+    sequential layers, ModificationLayer.py:5-24, 233-302; D_and_G_model.py:409-435), that
+    consumer's input-gradient launch already produces the whole gradient of y at its own
+    output pixels, and it reads y there (y is its input x): its epilogue writes
+    dx * act'(x) (desc.in_act), and the producer's backward takes that as g.
+
+    The producer creates the token (act, slope, its output y); the consumer's caller asserts
+    exclusivity (conv2d(act_in_ok=True)); the consumer's backward sets `pre` to the gradient
+    it wrote; the producer's backward checks that the gradient it received is that tensor.
+    Every path that does not apply it (double backward, three-call mode, a consumer whose
+    shortcut gradient went through autograd) leaves `pre` unset, and the producer masks as
+    before."""
+    __slots__ = ("act", "slope", "pre", "y")
+
+    def __init__(self, act, slope):
+        # (y: a weak reference -- the output carries the token, a strong one would be a cycle)
+        self.act, self.slope, self.pre, self.y = act, slope, None, None
+
+
+ACT_LINK = {"enabled": True}  # (A/B, tests: off = every conv masks its own gradient)
+
+
+@contextlib.contextmanager
+def act_links(on=True):
+    """Enable / disable ActToken links for the convs run inside (the WGAN-GP forward of
+    D(x_hat) disables them: its saved outputs also feed the double backward)."""
+    prev = ACT_LINK["enabled"]
+    ACT_LINK["enabled"] = bool(on)
+    try:
+        yield
+    finally:
+        ACT_LINK["enabled"] = prev
+
+
+def _act_out_taken(ctx, gy, allowed=True):
+    """True when the consumer of this conv's output already applied its act' (ActToken)."""
+    tok = getattr(ctx, "act_out", None)
+    if tok is None or tok.pre is None:
+        return False
+    pre, tok.pre = tok.pre, None
+    if not allowed:
+        raise RuntimeError("ActToken: a linked consumer applied act' but this backward cannot take it")
+    if pre.data_ptr() != gy.data_ptr() or tuple(pre.shape) != tuple(gy.shape):
+        raise RuntimeError("ActToken: the output gradient of a linked conv is not its consumer's input gradient "
+                           "alone (another consumer's gradient was summed in): act_in_ok was asserted wrongly")
+    return True
 
 
 # ---- launch groups: one node for the same layer of several independent networks (the four
@@ -1136,7 +1248,7 @@ class _ConvActGroup(torch.autograd.Function):
                 x, w, b, r = flat[4 * m:4 * m + 4]
                 lib.tpg_group_member()
                 sc = _MemberCtx()
-                outs.append(_conv_act_forward(sc, x, w, b, r, *sp, keep=keep))
+                outs.append(_conv_act_forward(sc, x, w, b, r, *sp[:7], keep=keep, links=sp[7]))
                 subs.append(sc)
         finally:
             rc = lib.tpg_group_end()
@@ -1196,9 +1308,12 @@ def conv2d_group(calls):
         geom = ConvGeom(weight.shape[2], weight.shape[3], c.get("stride", (1, 1)), c.get("pad", (0, 0, 0, 0)),
                         c.get("pad_mode", PAD_ZERO), c.get("transposed", False), c.get("output_padding", (0, 0)))
         specs.append((geom, code[0], code[1], float(c.get("res_scale", 1.0)), c.get("wparam"), c.get("link_res"),
-                      c.get("link_dx")))
+                      c.get("link_dx"), _act_links(c["x"], code, c.get("act_in_ok", False))))
         flat += [c["x"], weight, c.get("bias"), c.get("residual")]
-    return list(_ConvActGroup.apply(specs, *flat))
+    outs = list(_ConvActGroup.apply(specs, *flat))
+    for sp, y in zip(specs, outs):
+        _set_act_token(sp[7], y)
+    return outs
 
 
 RES_LINK = {"enabled": True}  # (A/B, tests: off = autograd sums it)

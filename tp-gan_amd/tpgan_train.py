@@ -663,7 +663,10 @@ class TPGANTrainer:
         flags = [p.requires_grad for p in params]
         set_requires_grad(params, False)
         try:
-            d_hat = self.D(x_hat).float()
+            # (no ActToken links: D's saved outputs of this forward also feed the double backward,
+            # so their gradients have more than one contribution)
+            with tpgan_ops.act_links(False):
+                d_hat = self.D(x_hat).float()
         finally:
             for p, f in zip(params, flags):
                 p.requires_grad_(f)
