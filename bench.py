@@ -40,8 +40,10 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 / fp16 MFMA (MI355X_MICROARCH.md, chip table; fp32 mode: same denominator)
 PEAK_HBM_GBS = 8000.0
 PROBED = ("fwd", "bwd", "wgrad")
-PASS_KERNEL = {"fwd": "halo_kernel forward", "bwd": "halo_kernel input gradient (masked: act' applied in the halo "
-                                                    "staging)", "wgrad": "wgrad_rh_kernel weight gradient (+ bias)"}
+PASS_KERNEL = {"fwd": "halo_kernel forward",
+               "bwd": "halo_kernel input gradient (gy arrives premasked by the consumer's epilogue; its own epilogue "
+                      "applies the producer's act' (in_act) or accumulates into the parked shortcut gradient)",
+               "wgrad": "wgrad_rh_kernel weight gradient (+ bias)"}
 
 
 def parse():
@@ -120,7 +122,7 @@ def main():
     batch = tpgan_train.synthetic_batch(B, dev, seed=1000 + rank, img_size=S)
 
     # dominant-kernel probes: enhance_features_128 (206 -> 206, 5x5, at the full face size), its
-    # forward, input gradient (the fused backward's first call: masked halo dgrad) and weight
+    # forward, input gradient (the fused backward's first call: round 5 act links) and weight
     # gradient -- the step's three largest kernels; `roofline` reports the one with the most
     # time per step (profiles/r04/kernel_trace_summary.txt: the weight gradient)
     def match(d, which):

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
 import torch  # noqa: E402
 
 import tpgan_ops as T  # noqa: E402
-from tpgan_lib import ACT_LEAKY, ACT_NONE, ACT_RELU, OP_BWD_DATA, OP_FWD, check, load, stream_ptr, tt  # noqa: E402
+from tpgan_lib import ACT_LEAKY, ACT_NONE, ACT_RELU, FLAG_DX_ACCUM, OP_BWD_DATA, OP_FWD, check, load, stream_ptr, tt  # noqa: E402
 
 # name: (N, Cin, H, W, Cout, k, stride, pad, transposed, output_padding, act, residual)
 SHAPES = {
@@ -122,7 +122,7 @@ def timed(fn, iters, graph):
     return e0.elapsed_time(e1) / iters
 
 
-def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=()):
+def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=(), dalgo=0):
     lib = load()
     dev = torch.device("cuda", 0)
     N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
@@ -141,11 +141,19 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=())
     dx = T.new_act(N, Cin, H, W, dt, dev)
     dw = torch.zeros_like(w)
     d = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
+    d.data_algo = dalgo  # (0: the planner's rule; 1 halo, 2 pointwise tap-DMA kernel)
     wd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
     wd.algo, wd.ksplit = wg_algo  # ((0, 0): the library's untuned default)
     if wg_algo == (0, 0) and T.AUTOTUNE["cache"]:  # --tune-file: the step's own pick for this shape
         wd.algo, wd.ksplit = T.AUTOTUNE["cache"].get(T._wgrad_key(wd), (0, 0))
     gd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)  # fused backward, input gradient only
+    # the step's input-gradient modes since round 5 (act links): gy arrives premasked, the
+    # epilogue applies the producer's act'(x) (desc.in_act) or adds into the parked shortcut
+    # gradient (TPG_FLAG_DX_ACCUM) -- enhance_128's two dgrads per step are one of each
+    xd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, ACT_NONE, 0.01, 1.0)
+    xd.in_act, xd.in_slope = ACT_LEAKY, 0.01
+    ad = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, ACT_NONE, 0.01, 1.0)
+    ad.flags |= FLAG_DX_ACCUM
     wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
     wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
     calls = {
@@ -159,6 +167,10 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=())
         # input gradient's halo (masked mode) where the geometry allows
         "bwd": lambda: check(lib.tpg_conv2d_bwd(ctypes.byref(gd), tt(x), tt(w), tt(y), tt(gy), tt(g), tt(dx),
                                                 tt(None), None, wsd.data_ptr(), wsd.numel(), stream_ptr())),
+        "dgxa": lambda: check(lib.tpg_conv2d_bwd(ctypes.byref(xd), tt(x), tt(w), tt(None), tt(gy), tt(None), tt(dx),
+                                                 tt(None), None, wsd.data_ptr(), wsd.numel(), stream_ptr())),
+        "dgacc": lambda: check(lib.tpg_conv2d_bwd(ctypes.byref(ad), tt(x), tt(w), tt(None), tt(gy), tt(None), tt(dx),
+                                                  tt(None), None, wsd.data_ptr(), wsd.numel(), stream_ptr())),
     }
     f = flops(s)
     if sweep:  # every weight-gradient (algo, pixel split) the tuner would try
@@ -217,6 +229,7 @@ def main():
     ap.add_argument("--graph", action="store_true", help="time graph replays (GPU time of short kernels)")
     ap.add_argument("--r50", action="store_true", help="the ResNet-50 identity extractor's shapes (configs[2])")
     ap.add_argument("--dsplits", default="", help="also time forced fwd / dgrad k splits, e.g. 1,2,4,8")
+    ap.add_argument("--dalgo", type=int, default=0, help="forward / input-gradient kernel (desc.data_algo)")
     ap.add_argument("--tune-file", default=None,
                     help="weight-gradient picks saved by a train step (bench.py with TPG_TUNE_DUMP=path)")
     a = ap.parse_args()
@@ -230,7 +243,7 @@ def main():
         algos = dict(kv.split("=") for kv in a.wg_algo.split(",") if kv)
         al = algos.get(name, "0").split("/")
         run(name, s, a.iters, a.passes.split(","), a.wg_sweep, (int(al[0]), int(al[1]) if len(al) > 1 else 0),
-            a.graph, ds)
+            a.graph, ds, a.dalgo)
 
 
 if __name__ == "__main__":

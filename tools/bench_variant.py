@@ -1,0 +1,27 @@
+"""bench.py with tpgan_ops module switches set first (for same-box kernel-trace A/Bs under
+rocprofv3, which must launch python3 on a script directly):
+
+    python tools/bench_variant.py CAT_LINK=0 ACT_LINK=1 -- --steps 10 --warmup 5 --no-cpu-baseline
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "tp-gan_amd")]
+
+
+def main():
+    argv = sys.argv[1:]
+    sets = argv[:argv.index("--")] if "--" in argv else argv
+    rest = argv[argv.index("--") + 1:] if "--" in argv else []
+    import tpgan_ops
+    for kv in sets:
+        k, v = kv.split("=")
+        getattr(tpgan_ops, k)["enabled"] = bool(int(v))
+    sys.argv = [os.path.join(REPO, "bench.py")] + rest
+    import bench
+    bench.main()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,115 @@
+"""Where a small-map conv kernel's time goes, block by block (ablation build only).
+
+    make -C tp-gan_amd ablate ABL_SRCS="tpg_halo tpg_pw" VARIANT=-DTPG_BLOCK_TIMING ADIR=abl/tl
+    TPG_LIB_PATH=tp-gan_amd/abl/tl/libtpgan_hip.so python tools/block_timeline.py \
+        --only conv4_res,local_10 --passes fwd,dgrad [--dalgo 2] [--dsplit 4]
+
+Thread 0 of every halo / pointwise block stores s_memrealtime (100 MHz, one clock for the whole
+chip) at entry (t0), before the main loop (t1), after it (t2) and after the epilogue (t3).  Per
+launch: the kernel span (first t0 to last t3), the spread of block start times (dispatch ramp),
+and the per-block prologue / main loop / epilogue durations, in microseconds.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+import torch  # noqa: E402
+
+import tpgan_ops as T  # noqa: E402
+from bench_layers import SHAPES  # noqa: E402
+from tpgan_lib import ACT_LEAKY, OP_BWD_DATA, OP_FWD, check, load, stream_ptr, tt  # noqa: E402
+
+CAP = 1 << 16  # blocks
+
+
+def pct(v, q):
+    v = sorted(v)
+    return v[min(len(v) - 1, int(q * (len(v) - 1) + 0.5))]
+
+
+def run(name, s, passes, dalgo, dsplit, buf, lib):
+    dev = torch.device("cuda", 0)
+    N, Cin, H, W, Cout, k, st, p, tr, op, act, use_res = s
+    dt = torch.bfloat16
+    geom = T.ConvGeom(k, k, (st, st), (p, p, p, p), 0, tr, (op, op))
+    OH, OW = geom.out_hw(H, W)
+    x = T.new_act(N, Cin, H, W, dt, dev).normal_()
+    w = (torch.randn((Cin, Cout, k, k) if tr else (Cout, Cin, k, k), device=dev) * 0.05).contiguous(
+        memory_format=torch.channels_last)
+    b = torch.zeros(Cout, device=dev)
+    y = T.new_act(N, Cout, OH, OW, dt, dev)
+    res = T.new_act(N, Cout, OH, OW, dt, dev).normal_() if use_res else None
+    g = T.new_act(N, Cout, OH, OW, dt, dev).normal_()
+    dx = T.new_act(N, Cin, H, W, dt, dev)
+    d = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
+    d.data_algo, d.data_ksplit = dalgo, dsplit
+    wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
+    wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
+    calls = {
+        "fwd": lambda: check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w), b.data_ptr() if act else None,
+                                                tt(res), tt(y), wsf.data_ptr(), wsf.numel(), stream_ptr())),
+        "dgrad": lambda: check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w), tt(dx), wsd.data_ptr(),
+                                                       wsd.numel(), stream_ptr())),
+    }
+    for kind in passes:
+        fn = calls[kind]
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        call_us = e0.elapsed_time(e1) * 1e3
+        buf.zero_()
+        torch.cuda.synchronize()
+        fn()
+        torch.cuda.synchronize()
+        t = buf.view(-1, 4).cpu()
+        t = t[t[:, 0] != 0].double() * 0.01  # 100 MHz ticks -> us
+        if t.numel() == 0:
+            print("%-10s %-5s no instrumented blocks" % (name, kind), flush=True)
+            continue
+        T0 = t[:, 0].min().item()
+        span = t[:, 3].max().item() - T0
+        start = (t[:, 0] - T0).tolist()
+        pro = (t[:, 1] - t[:, 0]).tolist()
+        loop = (t[:, 2] - t[:, 1]).tolist()
+        epi = (t[:, 3] - t[:, 2]).tolist()
+        first_end = t[:, 3].min().item() - T0
+        late = sum(1 for v in start if v > first_end)
+        print("%-10s %-5s algo %d ks %d | call %.1f us  span %.1f  blocks %d (started after the first ended: %d) | "
+              "start p50 %.1f p90 %.1f max %.1f | prologue %.1f/%.1f  loop %.1f/%.1f  epilogue %.1f/%.1f (mean/max)"
+              % (name, kind, dalgo, dsplit, call_us, span, t.shape[0], late, pct(start, .5), pct(start, .9),
+                 max(start), sum(pro) / len(pro), max(pro), sum(loop) / len(loop), max(loop),
+                 sum(epi) / len(epi), max(epi)), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", required=True)
+    ap.add_argument("--passes", default="fwd,dgrad")
+    ap.add_argument("--dalgo", default="0", help="comma list of desc.data_algo values")
+    ap.add_argument("--dsplit", default="0", help="comma list of desc.data_ksplit values")
+    a = ap.parse_args()
+    lib = load()
+    if not (hasattr(lib, "tpg_abl_tl_pw") and hasattr(lib, "tpg_abl_tl_halo")):
+        raise SystemExit("needs the -DTPG_BLOCK_TIMING ablation build (TPG_LIB_PATH)")
+    buf = torch.zeros(CAP * 4, dtype=torch.int64, device="cuda")
+    for f in (lib.tpg_abl_tl_pw, lib.tpg_abl_tl_halo):
+        f.argtypes = [ctypes.c_void_p]
+        assert f(buf.data_ptr()) == 0
+    for name in a.only.split(","):
+        for al in (int(v) for v in a.dalgo.split(",")):
+            for ks in (int(v) for v in a.dsplit.split(",")):
+                run(name, SHAPES[name], a.passes.split(","), al, ks, buf, lib)
+
+
+if __name__ == "__main__":
+    main()

@@ -93,8 +93,11 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
 #endif
 
 
+TPG_TL_DEFINE(halo)
+
 template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
 __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> GA) {
+  TPG_TL_MARK(0);
   // block -> (member, x = sub-tile group, y = N-tile, z = k split); a grouped grid is 1-D in
   // the plain grid's dispatch order (x fastest) within each member
   int mem = 0, bx, by, bz;
@@ -407,6 +410,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     if constexpr (MASK) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // y chunks landed
     store_halo(0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    TPG_TL_MARK(1);
     int ks = 0, t = 0, slot = 0;
     int toff = s_toff[0];
     for (int s = 0; s < total; ++s) {
@@ -434,6 +438,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
   }
+  TPG_TL_MARK(2);
 
   if (lag) held_mfmas();  // the last step's carried MFMAs
 
@@ -583,7 +588,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
             for (int e = 0; e < 8; ++e) xx.e[e] = e < ncol ? xs[e] : (E)0.f;
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope);
+          for (int e = 0; e < 8; ++e)
+            o.e[e] = (E)tpg_xa_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope, p.xa_segs, min(col0 + e, p.Nout - 1));
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) o.e[e] = (E)h_act(v[e], p.act, p.slope);
@@ -601,6 +607,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     }
     if (pass + 1 < BM / RP) __syncthreads();  // before the next pass overwrites s_acc
   }
+#ifdef TPG_BLOCK_TIMING
+  __syncthreads();
+  TPG_TL_MARK(3);
+#endif
 }
 
 // {id, HL, BN, WM, WN}; id = 8 * (HL - 3) + bn index.  BN 80 serves the 75 / 80-channel layers.  BN 208 (13 fragments on one wave

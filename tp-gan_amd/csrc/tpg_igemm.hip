@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
             E o;
             if (XA) {
               const unsigned short x16 = (unsigned short)(e ? (xh >> 16) : (xh & 0xffffu));
-              o = (E)tpg_act_grad(x, (float)__builtin_bit_cast(E, x16), p.xa_act, p.xa_slope);
+              o = (E)tpg_xa_grad(x, (float)__builtin_bit_cast(E, x16), p.xa_act, p.xa_slope, p.xa_segs, col + u);
             } else {
               o = (E)act_apply(x, p.act, p.slope);
             }
@@ -354,7 +354,8 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
       float x = v[u];
       if (p.bias) x += p.bias[p.bias_mod ? (col + u) % p.bias_mod : col + u];
       if (R) x += p.res_scale * ld_f(R + ro + u);
-      st_f(Y + yo + u, XA ? tpg_act_grad(x, ld_f(XA + yo + u), p.xa_act, p.xa_slope) : act_apply(x, p.act, p.slope));
+      st_f(Y + yo + u, XA ? tpg_xa_grad(x, ld_f(XA + yo + u), p.xa_act, p.xa_slope, p.xa_segs, col + u)
+                          : act_apply(x, p.act, p.slope));
     }
   }
 }

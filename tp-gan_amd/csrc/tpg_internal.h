@@ -55,6 +55,25 @@ __device__ __forceinline__ float tpg_act_grad(float g, float y, int act, float s
   return g;
 }
 
+// per-channel-segment slopes of desc.in_act = TPG_ACT_CHANNEL (kernel arguments: no loads)
+struct XaSegs {
+  int nseg;
+  int end[4];
+  float slope[4];
+};
+
+// the input-gradient epilogue's producer act' (desc.in_act): a segment slope when nseg > 0
+__device__ __forceinline__ float tpg_xa_grad(float g, float x, int act, float slope, const XaSegs& sg, int c) {
+  if (sg.nseg > 0) {
+    float s = sg.slope[3];
+    s = c < sg.end[2] ? sg.slope[2] : s;
+    s = c < sg.end[1] ? sg.slope[1] : s;
+    s = c < sg.end[0] ? sg.slope[0] : s;
+    return x > 0.f ? g : g * s;
+  }
+  return tpg_act_grad(g, x, act, slope);
+}
+
 // Fast unsigned division by a runtime constant for n, d < 2^31 (round-up method):
 // s = ceil(log2 d), mul = ceil(2^(31+s) / d) < 2^32, q = umulhi(n, mul) >> (s - 1).
 struct FastDiv {
@@ -80,6 +99,27 @@ struct FastDiv {
 // pipeline step instead of a counted wait on that step's fragment reads.  Callers order the
 // DMA'd bytes themselves (s_waitcnt vmcnt + s_barrier); the pass, not seeing these loads, only
 // ever waits for more VMEM operations than it needs (in-order completion), never fewer.
+// Per-block timeline (ablation builds only, -DTPG_BLOCK_TIMING; tools/block_timeline.py): thread 0
+// of every block stores s_memrealtime (100 MHz) at kernel entry, before the main loop, after it
+// and at the end, into the buffer a per-file tpg_abl_tl_<file>() set (vector stores).
+#ifdef TPG_BLOCK_TIMING
+#define TPG_TL_DEFINE(NAME)                                                                    \
+  __device__ unsigned long long* g_tl_buf = nullptr;                                          \
+  extern "C" int tpg_abl_tl_##NAME(void* buf) {                                               \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_tl_buf), &buf, sizeof(buf));                   \
+  }
+#define TPG_TL_MARK(i)                                                                         \
+  do {                                                                                         \
+    unsigned long long* b_ = g_tl_buf;                                                         \
+    if (b_ && threadIdx.x == 0)                                                                \
+      b_[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + (i)] =         \
+          __builtin_amdgcn_s_memrealtime();                                                    \
+  } while (0)
+#else
+#define TPG_TL_DEFINE(NAME)
+#define TPG_TL_MARK(i) do {} while (0)
+#endif
+
 __device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_base) {
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(lds_base));  // (M0 -> LDS-DMA: 1 wait state)
 }
@@ -334,6 +374,22 @@ __device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bn
 
 int launch_pack_many(const PackJob* jobs_dev, int n, int nblocks, hipStream_t s);
 
+// Adam fused with the packing of each parameter's owner image (tpg_adam_pack_run)
+constexpr int TPG_ADAM_RANGE_BLOCK = 4096;  // elements per block of a range job
+struct AdamPackJob {
+  PackJob pj;                 // owner: a halo-layout image with unit channel stride (pj.k.W in the params)
+  int kind;                   // 0: element range, 1: owner image
+  int64_t off, len;           // range: flat elements [off, off + len); owner: len = parameter chunks
+  int first_block, nblocks;
+};
+int launch_adam_pack(const AdamPackJob* jobs, int n, int nblocks, float* p, const float* g, float* m, float* v,
+                     float lr, float b1, float b2, float eps, float wd, const float* st, float gscale, hipStream_t s);
+int launch_adam_sched(float* st, float b1, float b2, int host_step, hipStream_t s);
+// dx[p][c] *= (x[p][c] > 0 ? 1 : slopes[c]) in place (desc.in_act TPG_ACT_CHANNEL, plans whose
+// epilogue cannot apply it)
+int launch_act_chan_inplace(int n, int c, int h, int w, const tpg_tensor& x, const tpg_tensor& dx, const XaSegs& sg,
+                            hipStream_t s);
+
 struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [+ res])
   const float* ws;
   int nslices;                // number of partial slices (1 for atomically accumulated ws)
@@ -354,6 +410,7 @@ struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [
   const void* XA;
   int xa_act;
   float xa_slope;
+  XaSegs xa_segs;             // per-channel-segment slopes (TPG_ACT_CHANNEL: nseg > 0)
 };
 
 // ---------------------------------------------------------------- halo direct conv ----
@@ -402,6 +459,7 @@ struct HaloArgs {
   const void* XA;
   int xa_act;
   float xa_slope;
+  XaSegs xa_segs;             // TPG_ACT_CHANNEL (nseg > 0): x > 0 ? v : v * the channel's segment slope
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 

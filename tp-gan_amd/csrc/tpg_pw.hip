@@ -21,7 +21,9 @@
 
 namespace tpg {
 
+#ifndef PW_NST
 #define PW_NST 4  // LDS ring stages (three k-steps in flight)
+#endif
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
@@ -40,17 +42,15 @@ __host__ __device__ constexpr int pw_lds_bytes(int bm, int bn) {
 
 template <int N_>
 __device__ __forceinline__ void pw_wait_vm() {
-  if constexpr (N_ <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N_ == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N_ == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N_ == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N_ == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N_ == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else static_assert(N_ == 8, "vmcnt");
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
+
+TPG_TL_DEFINE(pw)
 
 template <int DT, int BM, int BN>
 __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
+  TPG_TL_MARK(0);
   using E = dt_t<DT>;
   static_assert(DT == 1 || DT == 2, "16-bit operands");
   constexpr int KS = 32;                        // channels per k-step (64 bytes)
@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   __syncthreads();  // (tap table)
+  TPG_TL_MARK(1);
   if (total > 0) {
     // issue cursor (iks, it): the step NST - 1 ahead of the one computed, held at the last step
     int iks = 0, it = 0;
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the clamped tail DMAs)
   }
+  TPG_TL_MARK(2);
 
   // ---- epilogue through LDS (the halo kernel's): rows parked as fp32, then 8-channel groups
   constexpr int LDW = BN + 4, CG = BN / 8, NV = 8 * (int)sizeof(E) / 16;
@@ -279,7 +281,8 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
         for (int e = 0; e < 8; ++e) xx.e[e] = e < ncol ? xs[e] : (E)0.f;
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope);
+      for (int e = 0; e < 8; ++e)
+        o.e[e] = (E)tpg_xa_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope, p.xa_segs, min(col0 + e, p.Nout - 1));
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act(v[e], p.act, p.slope);
@@ -294,6 +297,10 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
         if (e < ncol) dst[e] = o.e[e];
     }
   }
+#ifdef TPG_BLOCK_TIMING
+  __syncthreads();
+  TPG_TL_MARK(3);
+#endif
 }
 
 // tile configs {bm, bn}: pw_cfg = 1 + index

@@ -110,12 +110,17 @@ class FlatParams:
         self.step += 1
         if check_finite:
             tpgan_ops.grad_check(self.grad, self.adam_state)
-        tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
-                            weight_decay, self.adam_state, 0, grad_scale)
+        fused = tpgan_ops.FUSED_ADAM_PACK["enabled"] and self.data.is_cuda and tpgan_ops.PACK["enabled"]
+        if not fused:
+            tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
+                                weight_decay, self.adam_state, 0, grad_scale)
         if check_finite:  # (on the device: no synchronisation; skipped_steps() reads it)
             self.skipped.add_(self.adam_state[3].ne(0).float())
         self.epoch += 1
-        tpgan_ops.repack(self)
+        if fused:  # (the update and the weight images in one launch; the skip check is the kernel's)
+            tpgan_ops.adam_pack(self, lr, betas[0], betas[1], eps, weight_decay, self.adam_state, 0, grad_scale)
+        else:
+            tpgan_ops.repack(self)
 
     def skipped_steps(self):
         """Updates skipped for non-finite gradients so far (synchronises).  A run whose static
@@ -886,6 +891,9 @@ class TPGANTrainer:
         # steps updated G bucket by bucket and never needed it); the images are re-packed unchanged
         tpgan_ops.repack(self.fG)
         tpgan_ops.repack(self.fD)
+        if tpgan_ops.FUSED_ADAM_PACK["enabled"]:
+            for f in (self.fG, self.fD):  # (the fused update's job tables: host -> device copies)
+                tpgan_ops._adam_pack_table(f)
         torch.cuda.synchronize()
         self._capturing = True  # graph replays reduce G in one call between phases
         self._segmented = bool(segmented)
