@@ -1,10 +1,10 @@
 """Where a small-map conv kernel's time goes, block by block (ablation build only).
 
-    make -C tp-gan_amd ablate ABL_SRCS="tpg_halo tpg_pw" VARIANT=-DTPG_BLOCK_TIMING ADIR=abl/tl
+    make -C tp-gan_amd ablate ABL_SRCS="tpg_halo tpg_pw tpg_wgrad2" VARIANT=-DTPG_BLOCK_TIMING ADIR=abl/tl
     TPG_LIB_PATH=tp-gan_amd/abl/tl/libtpgan_hip.so python tools/block_timeline.py \
-        --only conv4_res,local_10 --passes fwd,dgrad [--dalgo 2] [--dsplit 4]
+        --only conv4_res,local_10 --passes fwd,dgrad,wgrad [--dalgo 2] [--dsplit 4]
 
-Thread 0 of every halo / pointwise block stores s_memrealtime (100 MHz, one clock for the whole
+Thread 0 of every halo / pointwise / wgrad2 block stores s_memrealtime (100 MHz, one clock for the whole
 chip) at entry (t0), before the main loop (t1), after it (t2) and after the epilogue (t3).  Per
 launch: the kernel span (first t0 to last t3), the spread of block start times (dispatch ramp),
 and the per-block prologue / main loop / epilogue durations, in microseconds.
@@ -50,7 +50,13 @@ def run(name, s, passes, dalgo, dsplit, buf, lib):
     d.data_algo, d.data_ksplit = dalgo, dsplit
     wsf = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_FWD), dtype=torch.uint8, device=dev)
     wsd = torch.empty(lib.tpg_conv2d_workspace(ctypes.byref(d), OP_BWD_DATA), dtype=torch.uint8, device=dev)
+    dw = torch.zeros_like(w)
+    wd = geom.desc(N, Cin, H, W, Cout, OH, OW, dt, act, 0.01, 1.0)
+    if T.AUTOTUNE["cache"]:  # --tune-file: the step's own weight-gradient pick for this shape
+        wd.algo, wd.ksplit = T.AUTOTUNE["cache"].get(T._wgrad_key(wd), (0, 0))
     calls = {
+        "wgrad": lambda: check(lib.tpg_conv2d_bwd_filter(ctypes.byref(wd), tt(x), tt(g), tt(dw), None, 0,
+                                                         stream_ptr())),
         "fwd": lambda: check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w), b.data_ptr() if act else None,
                                                 tt(res), tt(y), wsf.data_ptr(), wsf.numel(), stream_ptr())),
         "dgrad": lambda: check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w), tt(dx), wsd.data_ptr(),
@@ -97,12 +103,15 @@ def main():
     ap.add_argument("--passes", default="fwd,dgrad")
     ap.add_argument("--dalgo", default="0", help="comma list of desc.data_algo values")
     ap.add_argument("--dsplit", default="0", help="comma list of desc.data_ksplit values")
+    ap.add_argument("--tune-file", default=None, help="weight-gradient picks saved by a train step (TPG_TUNE_DUMP)")
     a = ap.parse_args()
     lib = load()
     if not (hasattr(lib, "tpg_abl_tl_pw") and hasattr(lib, "tpg_abl_tl_halo")):
         raise SystemExit("needs the -DTPG_BLOCK_TIMING ablation build (TPG_LIB_PATH)")
+    if a.tune_file:
+        T.load_tuning(a.tune_file)
     buf = torch.zeros(CAP * 4, dtype=torch.int64, device="cuda")
-    for f in (lib.tpg_abl_tl_pw, lib.tpg_abl_tl_halo):
+    for f in [getattr(lib, n) for n in ("tpg_abl_tl_pw", "tpg_abl_tl_halo", "tpg_abl_tl_wgrad2") if hasattr(lib, n)]:
         f.argtypes = [ctypes.c_void_p]
         assert f(buf.data_ptr()) == 0
     for name in a.only.split(","):

@@ -832,6 +832,9 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     bool ok = xa->X.data && xa->X.dtype == Y.dtype && xa->X.stride[0] == Y.stride[0] && xa->X.stride[2] == Y.stride[2] &&
               xa->X.stride[3] == Y.stride[3] && xa->X.stride[1] == 1 && vec_ok(xa->X, dtype) == vec_ok(Y, dtype);
     for (const Prob& P : v) ok = ok && P.halo;
+    // (per-channel segment slopes, TPG_ACT_CHANNEL: not in the halo kernel's epilogue -- their
+    // per-element selects spilled its wide tiles -- so always the caller's in-place pass)
+    ok = ok && xa->segs.nseg == 0;
     if (ok) {
       XA = xa->X.data;
       xa->applied = true;

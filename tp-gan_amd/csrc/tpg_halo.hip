@@ -48,10 +48,20 @@ typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 __device__ __forceinline__ int hswz(int row) { return ((row >> 2) & 1) << 1; }
 
 __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 128; }
-// epilogue: rows of the 256-row tile parked in LDS per pass (fp32, stride BN + 4)
-__host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 80 ? 128 : 256; }
+// epilogue: rows of the 256-row tile parked in LDS per pass (fp32, stride BN + 4); 64 on the
+// 192..224-wide tiles, whose waves of the later passes still hold all their accumulators while
+// a pass is finished (128 rows put the 208 / 224 tiles with a producer-x epilogue past 256
+// VGPRs: ~700 B/lane of scratch spills, round 5)
+__host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 192 ? 64 : bn >= 80 ? 128 : 256; }
 // (row-offset table [BM][2] int64 + bias [256] floats, then the parked accumulator rows)
 __host__ __device__ constexpr int halo_epi_lds(int bn, int bm = 256) { return bm * 16 + 1024 + halo_epi_rows(bn) * (bn + 4) * 4; }
+// 256-row tiles (all small-map and grouped launches): the row-offset table and the bias live in
+// their own LDS region past both the main loop's buffers (`main` bytes) and the parked rows, so
+// the prologue fills them while its first loads are in flight and the epilogue's residual loads
+// can issue before the accumulators are parked
+__host__ __device__ constexpr int halo_epi_early_off(int main, int bn) {
+  return ((main > halo_epi_rows(bn) * (bn + 4) * 4 ? main : halo_epi_rows(bn) * (bn + 4) * 4) + 15) / 16 * 16;
+}
 
 // mask_chunk on a native 4 x u32 vector (first-class value: stays in VGPRs)
 template <int EPC>
@@ -100,13 +110,32 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   TPG_TL_MARK(0);
   // block -> (member, x = sub-tile group, y = N-tile, z = k split); a grouped grid is 1-D in
   // the plain grid's dispatch order (x fastest) within each member
+  // Small maps (several images per block, or a k split): the dispatch-order block index b runs
+  // on XCD b % 8; XCDs are handed contiguous ranges of the logical (x fastest) order, so each
+  // XCD runs every sub-tile of a few (N-tile, k split) pairs -- or of one grouped member -- and
+  // fetches their weight slices into its own L2 once (a 512-channel 3x3 layer's packed image is
+  // 4.7 MB, over one XCD's 4 MB L2, when every XCD streams all of it)
+  auto xcd_order = [](int b, int tot) {
+    const int full = tot & ~7;
+    return (tot >= 16 && b < full) ? (b & 7) * (full >> 3) + (b >> 3) : b;
+  };
   int mem = 0, bx, by, bz;
   if constexpr (NG == 1) {
     bx = blockIdx.x; by = blockIdx.y; bz = blockIdx.z;
+    const HaloArgs& q = GA.a[0];
+    if (!TPG_HALO_ROWMAJOR && !(q.IMG == 1 && gridDim.x >= 64 && (int)gridDim.x == q.N * q.tiles_h * q.tiles_w)) {
+      const int gx = gridDim.x, gy = gridDim.y;
+      const int L = xcd_order(bx + gx * (by + gy * bz), gx * gy * (int)gridDim.z);
+      bx = L % gx;
+      const int yz = L / gx;
+      by = yz % gy;
+      bz = yz / gy;
+    }
   } else {
-    mem = group_member(GA, blockIdx.x);
+    const int L = TPG_HALO_ROWMAJOR ? (int)blockIdx.x : xcd_order(blockIdx.x, gridDim.x);
+    mem = group_member(GA, L);
     const HaloArgs& q = GA.a[mem];
-    const int l = blockIdx.x - GA.boff[mem];
+    const int l = L - GA.boff[mem];
     const int gx = (q.N * q.tiles_h * q.tiles_w + q.IMG - 1) / q.IMG;
     const int yz = l / gx;
     bx = l - yz * gx;
@@ -149,6 +178,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   u32x4* halo = lds;                                   // [2][hcap][4]
   u32x4* wts = lds + 2 * hcap * 4;                     // [RS][BNL][4] ring
   int* s_toff = reinterpret_cast<int*>(wts + RS * BNL * 4);  // [TPG_MAX_TAPS]
+  constexpr bool EARLY = BM == 256;  // (see halo_epi_early_off)
+  const int e_base = halo_epi_early_off((2 * p.hcap * 4 + RS * BNL * 4) * 16 + TPG_MAX_TAPS * 4, BN);
+  int64_t* s_off = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(lds) + (EARLY ? e_base : 0));  // [BM][2]
+  float* s_bias = reinterpret_cast<float*>(s_off + 2 * BM);                                          // [256]
 
   const int tid = threadIdx.x;
   if (tid < TPG_MAX_TAPS) s_toff[tid] = p.toff[tid];
@@ -399,6 +432,38 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   //   end of s   : at t == ntaps-1 write the next halo to LDS; s_waitcnt vmcnt(GL)
   //                retires step s+1's DMA (issued during s-1) while step s+2's stays in
   //                flight; lgkmcnt(0); s_barrier.  Step s+1 then reads what was retired.
+  // epilogue row table: output / residual element offsets of each of the BM rows (-1 = no row),
+  // or the split-K slice row; and the bias of this block's columns
+  float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
+  auto epi_table = [&]() {
+    for (int q = tid; q < BM; q += 512) {
+      const int sub = q / THW, rem = q - sub * THW;
+      const int st = st0 + sub;
+      int64_t yo = -1, ro = 0;
+      if (sub < IMG && st < ntot) {
+        const int nimg = st / tiles, trem = st - nimg * tiles;
+        const int tty = trem / tiles_w, ttx = trem - tty * tiles_w;
+        const int ty = rem / TW, tx = rem - ty * TW;
+        const int j = tty * TH + ty, i = ttx * TW + tx;
+        if (j < p.JH && i < p.JW) {
+          if (W) {
+            yo = ((int64_t)(nimg * p.JH + j) * p.JW + i) * p.Nout;
+          } else {
+            const int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
+            yo = (int64_t)nimg * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
+            ro = (int64_t)nimg * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
+          }
+        }
+      }
+      s_off[2 * q] = yo;
+      s_off[2 * q + 1] = ro;
+    }
+    if (tid >= 512 - BN) {  // (the highest threads: BM >= 256 > BN)
+      const int c = n0 + tid - (512 - BN);
+      s_bias[tid - (512 - BN)] = (p.bias && c < p.Nout) ? p.bias[c] : 0.f;
+    }
+  };
+
   const int ntaps = p.ntaps;
   const int total = nks * ntaps;
   __syncthreads();  // tap table
@@ -407,6 +472,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     issue_m(0, 0);
     issue_w(0, 0);
     issue_w(min(1, total - 1), 1);
+    if constexpr (EARLY) epi_table();  // (while the first halo and weight loads are in flight)
     if constexpr (MASK) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // y chunks landed
     store_halo(0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -437,6 +503,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       if (++t == ntaps) { t = 0; ++ks; }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
+  } else if constexpr (EARLY) {
+    epi_table();
+    __syncthreads();
   }
   TPG_TL_MARK(2);
 
@@ -452,42 +521,46 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   constexpr int IPT = (RP * CG + 511) / 512;  // groups per thread per pass (the last partial)
   constexpr int NV = 8 * (int)sizeof(E) / 16;  // 16-byte vectors per group
   static_assert(RP % WTM == 0, "epilogue tiling");
-  __syncthreads();                           // every wave is done with the halo and the ring
-  int64_t* s_off = reinterpret_cast<int64_t*>(lds);           // [BM][2] out / residual offsets
-  float* s_bias = reinterpret_cast<float*>(lds) + BM * 4;     // [256] bias of this block's columns
-  float* s_acc = reinterpret_cast<float*>(lds) + BM * 4 + 256;  // [RP][LDW]
+  float* s_acc = reinterpret_cast<float*>(lds) + (EARLY ? 0 : BM * 4 + 256);  // [RP][LDW]
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
   const E* XA = reinterpret_cast<const E*>(p.XA);
-  float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
-  for (int q = tid; q < BM; q += 512) {
-    const int sub = q / THW, rem = q - sub * THW;
-    const int st = st0 + sub;
-    int64_t yo = -1, ro = 0;
-    if (sub < IMG && st < ntot) {
-      const int nimg = st / tiles, trem = st - nimg * tiles;
-      const int tty = trem / tiles_w, ttx = trem - tty * tiles_w;
-      const int ty = rem / TW, tx = rem - ty * TW;
-      const int j = tty * TH + ty, i = ttx * TW + tx;
-      if (j < p.JH && i < p.JW) {
-        if (W) {
-          yo = ((int64_t)(nimg * p.JH + j) * p.JW + i) * p.Nout;
-        } else {
-          const int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
-          yo = (int64_t)nimg * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw;
-          ro = (int64_t)nimg * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw;
-        }
-      }
+  // residual (or, without one, producer-x) vectors of a pass's groups: bf16 prefetches them,
+  // all loads in flight before the first wait; the fp32 parity mode and the rare residual +
+  // producer-x case (its x) load in the finishing loop.  One prefetch array: two (round 5's
+  // first in_act build) pushed the 208 / 224-wide tiles past 256 VGPRs into ~700 B/lane of
+  // scratch spills in the epilogue.
+  constexpr int PF = BF ? IPT : 0;
+  const bool pf_r = R != nullptr;
+  const E* PSRC = pf_r ? R : XA;
+  const bool pvec = pf_r ? p.rvec : p.yvec;
+  u32x4 pv[IPT][NV];
+  auto prefetch = [&](int pass) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < (PSRC ? PF : 0); ++k) {
+      const int it = min(tid + 512 * k, RP * CG - 1);  // clamped past the last group
+      const int row = it / CG, c0 = (it - row * CG) * 8;
+      // unconditional (clamped) loads so that all of them issue before the first wait
+      const int64_t yo = s_off[2 * (pass * RP + row)];
+      const bool ok = pvec && p.Nout - (n0 + c0) >= 8 && yo >= 0;
+      const u32x4* src = reinterpret_cast<const u32x4*>(PSRC + (ok ? (pf_r ? s_off[2 * (pass * RP + row) + 1] : yo) + n0 + c0 : 0));
+#pragma unroll
+      for (int v = 0; v < NV; ++v) pv[k][v] = src[v];
     }
-    s_off[2 * q] = yo;
-    s_off[2 * q + 1] = ro;
+  };
+  if constexpr (EARLY) {
+    // (the table is in its own region: pass 0's loads go out before the barrier that frees
+    // the halo / ring space for the parked rows)
+    if (!W) prefetch(0);
   }
-  if (tid >= 512 - BN) {  // (the highest threads: BM >= 256 > BN)
-    const int c = n0 + tid - (512 - BN);
-    s_bias[tid - (512 - BN)] = (p.bias && c < p.Nout) ? p.bias[c] : 0.f;
+  __syncthreads();                           // every wave is done with the halo and the ring
+  if constexpr (!EARLY) {
+    epi_table();
+    __syncthreads();
   }
 #pragma unroll 1
   for (int pass = 0; pass < BM / RP; ++pass) {
+    if (!W && (!EARLY || pass > 0)) prefetch(pass);  // (before the park: latency under the park + barrier)
     if (wm * WTM >= pass * RP && wm * WTM < (pass + 1) * RP) {
       float* base = s_acc + (wm * WTM - pass * RP + 4 * g) * LDW + wn * WTN + l16;  // constant offsets below
 #pragma unroll
@@ -521,31 +594,6 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         }
       }
     } else {
-      // residual vectors of every group first (all loads in flight), then finish and store
-      // (bf16; the fp32 parity mode loads them in the finishing loop: register budget)
-      constexpr int PF = BF ? IPT : 0;
-      u32x4 rv[IPT][NV], xv[IPT][NV];
-#pragma unroll
-      for (int k = 0; k < (R ? PF : 0); ++k) {
-        const int it = min(tid + 512 * k, RP * CG - 1);  // clamped past the last group
-        const int row = it / CG, c0 = (it - row * CG) * 8;
-        // unconditional (clamped) loads so that all of them issue before the first wait
-        const bool ok = p.rvec && p.Nout - (n0 + c0) >= 8 && s_off[2 * (pass * RP + row)] >= 0;
-        const u32x4* src = reinterpret_cast<const u32x4*>(R + (ok ? s_off[2 * (pass * RP + row) + 1] + n0 + c0 : 0));
-#pragma unroll
-        for (int v = 0; v < NV; ++v) rv[k][v] = src[v];
-      }
-      // desc.in_act: the producer's activation input x at the output's offsets (yvec: X has Y's
-      // strides and alignment), prefetched the same way
-#pragma unroll
-      for (int k = 0; k < (XA ? PF : 0); ++k) {
-        const int it = min(tid + 512 * k, RP * CG - 1);
-        const int row = it / CG, c0 = (it - row * CG) * 8;
-        const bool ok = p.yvec && p.Nout - (n0 + c0) >= 8 && s_off[2 * (pass * RP + row)] >= 0;
-        const u32x4* src = reinterpret_cast<const u32x4*>(XA + (ok ? s_off[2 * (pass * RP + row)] + n0 + c0 : 0));
-#pragma unroll
-        for (int v = 0; v < NV; ++v) xv[k][v] = src[v];
-      }
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const int it = tid + 512 * k;
@@ -568,7 +616,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         if (R) {
           union { u32x4 u[NV]; E e[8]; } rr;
 #pragma unroll
-          for (int q = 0; q < NV; ++q) rr.u[q] = rv[k][q];
+          for (int q = 0; q < NV; ++q) rr.u[q] = pv[k][q];
           if (!(full && p.rvec && BF)) {
             const E* rs = R + s_off[2 * (pass * RP + row) + 1] + col0;
 #pragma unroll
@@ -581,15 +629,19 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         if (XA) {  // input gradient for the producer: v * xa_act'(x)
           union { u32x4 u[NV]; E e[8]; } xx;
 #pragma unroll
-          for (int q = 0; q < NV; ++q) xx.u[q] = xv[k][q];
-          if (!(full && p.yvec && BF)) {
+          for (int q = 0; q < NV; ++q) xx.u[q] = pv[k][q];
+          if (pf_r && full && p.yvec && BF) {  // (residual prefetched: x loaded here)
+            const u32x4* xs = reinterpret_cast<const u32x4*>(XA + yo + col0);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) xx.u[q] = xs[q];
+          } else if (!(full && p.yvec && BF)) {
             const E* xs = XA + yo + col0;
 #pragma unroll
             for (int e = 0; e < 8; ++e) xx.e[e] = e < ncol ? xs[e] : (E)0.f;
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            o.e[e] = (E)tpg_xa_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope, p.xa_segs, min(col0 + e, p.Nout - 1));
+            o.e[e] = (E)tpg_act_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope);
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) o.e[e] = (E)h_act(v[e], p.act, p.slope);
@@ -664,7 +716,9 @@ int halo_cfg(int hl, int bn) {
 // 4-slot ring (-2..12 %: the second fragment set pushed the 224-wide tile past 256 VGPRs),
 // waves 4-7 at a raised priority (no gain; removed in round 4 with the other variant bits).
 size_t halo_lds_bytes(int hcap, int bn, int rs, int bm) {
-  return std::max((size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4, (size_t)halo_epi_lds(bn, bm));
+  const size_t main = (size_t)(2 * hcap * 4 + rs * halo_bnl(bn) * 4) * 16 + TPG_MAX_TAPS * 4;
+  if (bm == 256) return (size_t)halo_epi_early_off(main, bn) + bm * 16 + 1024;
+  return std::max(main, (size_t)halo_epi_lds(bn, bm));
 }
 
 template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>

@@ -459,7 +459,7 @@ struct HaloArgs {
   const void* XA;
   int xa_act;
   float xa_slope;
-  XaSegs xa_segs;             // TPG_ACT_CHANNEL (nseg > 0): x > 0 ? v : v * the channel's segment slope
+  XaSegs xa_segs;             // TPG_ACT_CHANNEL: never set for halo plans (run_probs; the pointwise epilogue reads it)
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 

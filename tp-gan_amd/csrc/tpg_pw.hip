@@ -64,13 +64,16 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int M = p.N * p.JH * p.JW;
   const int nmt = (M + BM - 1) / BM, nnt = (p.Nout + BN - 1) / BN;
-  // 1-D grid, (m-tile, n-tile) with the n-tiles of one m-tile consecutive; each XCD (physical
-  // block b on XCD b % 8) gets a contiguous range, so the tiles sharing A rows meet in one L2
-  const int per = nmt * nnt;
-  const int bid = blockIdx.x % per, z = blockIdx.x / per;
-  const int full = per & ~7;
-  const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
-  const int mt = L / nnt, nt = L - mt * nnt;
+  // 1-D grid over (m-tile, n-tile, k split), m-tiles fastest; each XCD (physical block b on XCD
+  // b % 8) gets a contiguous range, i.e. all m-tiles of a few (n-tile, split) pairs, so their
+  // weight slices -- the larger operand of these small-map GEMMs (4.7 MB for 512 -> 512 3x3,
+  // over one XCD's 4 MB L2) -- are fetched into that XCD's L2 once
+  const int per = nmt * nnt, tot = per * (int)(gridDim.x / per);
+  const int full = tot & ~7;
+  const int b = blockIdx.x;
+  const int L = (tot >= 16 && b < full) ? (b & 7) * (full >> 3) + (b >> 3) : b;
+  const int mt = L % nmt, rest = L / nmt;
+  const int nt = rest % nnt, z = rest / nnt;
   const int m0 = mt * BM, n0 = nt * BN;
   const int ks0 = z * p.kps;
   const int nks = min(p.nks, ks0 + p.kps) - ks0;
