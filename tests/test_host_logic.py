@@ -109,6 +109,8 @@ def test_tuning_file_roundtrip_and_old_keys(tmp_path):
         assert len(k0[1]) == len(k1[1]) == tpgan_ops._WGRAD_KEY_LEN and k0 != k1
         tpgan_ops.AUTOTUNE["cache"].clear()
         tpgan_ops.AUTOTUNE["cache"][k1] = (7, 4)
+        kd = ("dsplit", 1, tpgan_ops._desc_tuple(d) + (1, 2))  # (forward / input-gradient split picks)
+        tpgan_ops.AUTOTUNE["cache"][kd] = (4, 2)
         p = str(tmp_path / "tune.json")
         tpgan_ops.save_tuning(p)
         old = str(tmp_path / "old.json")
@@ -118,6 +120,7 @@ def test_tuning_file_roundtrip_and_old_keys(tmp_path):
         tpgan_ops.load_tuning(old)
         assert tpgan_ops.AUTOTUNE["cache"][k1] == (7, 4)
         assert tpgan_ops.AUTOTUNE["cache"][k0] == (12, 2)
+        assert tpgan_ops.AUTOTUNE["cache"][kd] == (4, 2)
     finally:
         tpgan_ops.AUTOTUNE["cache"].clear()
         tpgan_ops.AUTOTUNE["cache"].update(saved)

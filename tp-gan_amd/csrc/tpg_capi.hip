@@ -563,6 +563,9 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   h.pad_mode = a.pad_mode;
   h.N = N; h.JH = JH; h.JW = JW;
   h.tiles_h = cdiv(JH, bth); h.tiles_w = cdiv(JW, btw);
+  h.fd_hp.init(h.HH * h.HW); h.fd_hw.init(h.HW);
+  h.fd_tiles.init(h.tiles_h * h.tiles_w); h.fd_tilesw.init(h.tiles_w);
+  h.fd_thw.init(bth * btw); h.fd_tw.init(btw);
   h.BN = bn; h.ntiles = cdiv(a.Nout, bn); h.Nout = a.Nout;
   h.oy0 = a.oy0; h.ox0 = a.ox0; h.osy = a.osy; h.osx = a.osx;
   // split over k-steps until the grid covers the chip (each split >= 4 pipeline steps)

@@ -202,6 +202,28 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   const char* wsrc = reinterpret_cast<const char*>(p.Wp) + (int64_t)ks0 * p.ntaps * wstep +
                      (int64_t)by * BNL * 64 + (wave * GL * 1024 + lane * 16);
 
+  // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
+  // (the ring's LDS address and the step offset as 32-bit scalars: the generic-pointer form
+  // cost a 64-bit multiply, an address-space null check and two readfirstlanes per step)
+  const uint32_t wts_lds = __builtin_amdgcn_readfirstlane(lds_addr(wts)) +
+                           (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (GL * 1024);
+  const uint32_t wstep32 = (uint32_t)wstep;  // (packed image < 2^31 bytes: planner)
+  auto issue_w = [&](int step, int slot) {
+    if constexpr ((TPG_HALO_ABL & 1) != 0) return;
+    const char* src = wsrc + (uint32_t)step * wstep32;
+    const uint32_t d0 = wts_lds + (uint32_t)slot * (BNL * 64);
+#pragma unroll
+    for (int j = 0; j < GL; ++j) lds_dma16(src + j * 1024, d0 + j * 1024);
+  };
+
+  // the first two steps' weight DMAs go out before the halo index math (they need none of
+  // it), so their latency runs under it
+  const int total = nks * p.ntaps;
+  if (total > 0) {
+    issue_w(0, 0);
+    issue_w(min(1, total - 1), 1);
+  }
+
   // ---- per-thread halo slots (fixed across k-steps): element offset from A (absolute,
   // < 2^31 by the planner), negative = outside the image or a dead sub-tile -> zero
   int hoff[HL];
@@ -216,12 +238,12 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     hoff[q] = -1;
     if constexpr (MASK) mpix[q] = -1;
     if (hp < IMG * HP) {
-      const int sub = hp / HP, hl = hp - sub * HP;
+      const int sub = (int)p.fd_hp.div(hp), hl = hp - sub * HP;
       const int st = st0 + sub;
       if (st < ntot) {
-        const int nimg = st / tiles, trem = st - nimg * tiles;
-        const int ty = trem / tiles_w, tx = trem - ty * tiles_w;
-        const int hy = hl / HW, hx = hl - hy * HW;
+        const int nimg = (int)p.fd_tiles.div(st), trem = st - nimg * tiles;
+        const int ty = (int)p.fd_tilesw.div(trem), tx = trem - ty * tiles_w;
+        const int hy = (int)p.fd_hw.div(hl), hx = hl - hy * HW;
         int gy = ty * TH * SH + p.dymin + hy, gx = tx * TW * SW + p.dxmin + hx;
         if (p.pad_mode) { gy = h_refl(gy, p.A_H); gx = h_refl(gx, p.A_W); }
         bool real = true;
@@ -310,28 +332,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       }
     }
   };
-  // LDS-DMA of one step's weight slice into ring slot `slot` (GL pieces per wave)
-  // (the ring's LDS address and the step offset as 32-bit scalars: the generic-pointer form
-  // cost a 64-bit multiply, an address-space null check and two readfirstlanes per step)
-  const uint32_t wts_lds = __builtin_amdgcn_readfirstlane(lds_addr(wts)) +
-                           (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (GL * 1024);
-  const uint32_t wstep32 = (uint32_t)wstep;  // (packed image < 2^31 bytes: planner)
-  auto issue_w = [&](int step, int slot) {
-    if constexpr ((TPG_HALO_ABL & 1) != 0) return;
-    const char* src = wsrc + (uint32_t)step * wstep32;
-    const uint32_t d0 = wts_lds + (uint32_t)slot * (BNL * 64);
-#pragma unroll
-    for (int j = 0; j < GL; ++j) lds_dma16(src + j * 1024, d0 + j * 1024);
-  };
-
   const int wm = wave / WN, wn = wave % WN;
   const int l16 = lane & 15, g = lane >> 4, g16 = g << 4;
   int hbase[MREP];
 #pragma unroll
   for (int m = 0; m < MREP; ++m) {
     const int q = wm * WTM + m * 16 + l16;
-    const int sub = q / THW, rem = q - sub * THW;
-    const int ty = rem / TW, tx = rem - ty * TW;
+    const int sub = (int)p.fd_thw.div(q), rem = q - sub * THW;
+    const int ty = (int)p.fd_tw.div(rem), tx = rem - ty * TW;
     hbase[m] = sub < IMG ? sub * HP + ty * SH * HW + tx * SW : 0;  // dead rows read row 0
   }
   f32x4 acc[MREP][NREP];
@@ -437,13 +445,13 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
   auto epi_table = [&]() {
     for (int q = tid; q < BM; q += 512) {
-      const int sub = q / THW, rem = q - sub * THW;
+      const int sub = (int)p.fd_thw.div(q), rem = q - sub * THW;
       const int st = st0 + sub;
       int64_t yo = -1, ro = 0;
       if (sub < IMG && st < ntot) {
-        const int nimg = st / tiles, trem = st - nimg * tiles;
-        const int tty = trem / tiles_w, ttx = trem - tty * tiles_w;
-        const int ty = rem / TW, tx = rem - ty * TW;
+        const int nimg = (int)p.fd_tiles.div(st), trem = st - nimg * tiles;
+        const int tty = (int)p.fd_tilesw.div(trem), ttx = trem - tty * tiles_w;
+        const int ty = (int)p.fd_tw.div(rem), tx = rem - ty * TW;
         const int j = tty * TH + ty, i = ttx * TW + tx;
         if (j < p.JH && i < p.JW) {
           if (W) {
@@ -465,13 +473,10 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   };
 
   const int ntaps = p.ntaps;
-  const int total = nks * ntaps;
-  __syncthreads();  // tap table
+  // (the tap table written at entry is read only after the prologue's closing barrier)
   if (total > 0) {
     load_halo(0);
     issue_m(0, 0);
-    issue_w(0, 0);
-    issue_w(min(1, total - 1), 1);
     if constexpr (EARLY) epi_table();  // (while the first halo and weight loads are in flight)
     if constexpr (MASK) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // y chunks landed
     store_halo(0);

@@ -460,6 +460,10 @@ struct HaloArgs {
   int xa_act;
   float xa_slope;
   XaSegs xa_segs;             // TPG_ACT_CHANNEL: never set for halo plans (run_probs; the pointwise epilogue reads it)
+  // the prologue's index math by multiply-shift (each runtime division was ~25 VALU; the
+  // small-map blocks spent ~1-2 us of a ~5 us prologue on them): HH*HW, HW, tiles_h*tiles_w,
+  // tiles_w, TH*TW, TW
+  FastDiv fd_hp, fd_hw, fd_tiles, fd_tilesw, fd_thw, fd_tw;
   int toff[TPG_MAX_TAPS];     // per tap: (dy - dymin) * HW + (dx - dxmin), halo pixel shift
 };
 

@@ -65,8 +65,11 @@ __host__ __device__ constexpr int w2_stages(int dt, int bm, int bn) {
   return (TPG_W2_NST * (dt ? 64 * (bm + bn) * 2 : 32 * (bm + bn) * 4) <= 80 * 1024) ? TPG_W2_NST : 3;
 }
 
+TPG_TL_DEFINE(wgrad2)
+
 template <int DT, int BM, int BN, int WM, int WN, bool FLAT, int NG = 1>
 __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, NG> G) {
+  TPG_TL_MARK(0);
   // grouped launch: member m owns blocks [boff[m], boff[m + 1]) (its own 1-D grid)
   int mem = 0, bid0 = blockIdx.x, nblk0 = gridDim.x;
   if constexpr (NG > 1) {
@@ -387,6 +390,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
 #pragma unroll
     for (int j = 0; j < NST - 1; ++j) issue(min(j, nkt - 1), j);
     W2_WAIT_BARRIER();  // retires k-tile 0
+    TPG_TL_MARK(1);
     int slot = 0;
     for (int kt = 0; kt < nkt; ++kt) {
       const int slot2 = slot == 0 ? NST - 1 : slot - 1;
@@ -397,6 +401,7 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  TPG_TL_MARK(2);
 #undef W2_WAIT_BARRIER
 
   // ---- epilogue: the fp32 tile goes through LDS so that dW is written in whole rows.
@@ -407,7 +412,10 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
   //   sole owner (ksplit == 1): 16-byte read-add-write of 4 consecutive columns per thread;
   //   pixel split: one no-return atomic per lane, 64 lanes = 64 consecutive columns of ONE row
   //   (256 contiguous bytes per wave-instruction: the full-rate shape).
-  if (nkt <= 0) return;  // (an empty pixel split adds nothing; block-uniform)
+  if (nkt <= 0) {  // (an empty pixel split adds nothing; block-uniform)
+    TPG_TL_MARK(3);
+    return;
+  }
   if constexpr ((TPG_W2_ABL & 16) != 0) {
 #pragma unroll
     for (int m = 0; m < MREP; ++m) {
@@ -454,21 +462,34 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
   const int amax = min(BM, p.Ca - a0);
   if (p.ksplit == 1) {
     constexpr int CPR = BN / 4, RPP = 512 / CPR;  // 4-column chunks per row, rows per pass
+    constexpr int NIT = (BM + RPP - 1) / RPP;     // passes
     const int ch = tid % CPR, c0 = 4 * ch;
     int off[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) off[e] = col_off(c0 + e);
     const bool vec = p.w_sb == 1 && (p.w_sa & 3) == 0 && ((uintptr_t)p.dW & 15) == 0 && off[0] >= 0 &&
                      (off[0] & 3) == 0 && off[3] == off[0] + 3;
-    for (int row = tid / CPR; row < amax; row += RPP) {
+    if (vec) {
+      // every pass's dW chunk read first (one memory latency, not one per pass), then add + store
+      float4 o[NIT];
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const int row = tid / CPR + i * RPP;
+        if (row < amax) o[i] = *reinterpret_cast<const float4*>(p.dW + (a0 + row) * p.w_sa + off[0]);
+      }
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const int row = tid / CPR + i * RPP;
+        if (row >= amax) continue;
+        const float4 v = *reinterpret_cast<const float4*>(Cs + row * LDC + c0);
+        o[i].x += v.x; o[i].y += v.y; o[i].z += v.z; o[i].w += v.w;
+        *reinterpret_cast<float4*>(p.dW + (a0 + row) * p.w_sa + off[0]) = o[i];
+      }
+    }
+    for (int row = tid / CPR; !vec && row < amax; row += RPP) {
       const float4 v = *reinterpret_cast<const float4*>(Cs + row * LDC + c0);
       float* dst = p.dW + (a0 + row) * p.w_sa;
-      if (vec) {
-        float4* d4 = reinterpret_cast<float4*>(dst + off[0]);
-        float4 o = *d4;
-        o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
-        *d4 = o;
-      } else {
+      {
         if (off[0] >= 0) dst[off[0]] += v.x;
         if (off[1] >= 0) dst[off[1]] += v.y;
         if (off[2] >= 0) dst[off[2]] += v.z;
@@ -499,6 +520,10 @@ __global__ __launch_bounds__(512) void wgrad2_kernel(const Grouped<Wgrad2Args, N
         else atomicAdd(p.dbias + a, accb[m][reg]);
       }
   }
+#ifdef TPG_BLOCK_TIMING
+  __syncthreads();
+  TPG_TL_MARK(3);
+#endif
 }
 
 // {id, BM, BN, WM, WN}

@@ -290,9 +290,17 @@ def _desc_tuple(d):
 
 
 def save_tuning(path):
+    """Write the autotuner's picks: weight-gradient keys as [shape, "wgrad", pick], forward /
+    input-gradient split keys as [shape, "dsplit:<op>", pick]."""
     import json
+    rows = []
+    for k, v in AUTOTUNE["cache"].items():
+        if k[0] == "dsplit":
+            rows.append([list(k[2]), "dsplit:%d" % k[1], list(v)])
+        else:
+            rows.append([list(k[1]), k[0], list(v)])
     with open(path, "w") as f:
-        json.dump([[list(k[1]), k[0], v] for k, v in AUTOTUNE["cache"].items()], f)
+        json.dump(rows, f)
 
 
 _WGRAD_KEY_LEN = 19  # _desc_tuple (18 fields) + the concurrency flag
@@ -305,6 +313,9 @@ def load_tuning(path):
     with open(path) as f:
         for key, op, v in json.load(f):
             key = tuple(key)
+            if op.startswith("dsplit:"):
+                AUTOTUNE["cache"][("dsplit", int(op.split(":")[1]), key)] = tuple(v)
+                continue
             if len(key) == _WGRAD_KEY_LEN - 1:
                 key = key + (0,)
             elif len(key) != _WGRAD_KEY_LEN:
