@@ -27,6 +27,8 @@ SHAPES = {
     "add_128": (32, 75, 128, 128, 75, 7, 1, 3, False, 0, ACT_LEAKY, True),
     "conv0_res": (32, 64, 128, 128, 64, 7, 1, 3, False, 0, ACT_LEAKY, True),
     "conv5_0": (32, 206, 128, 128, 64, 5, 1, 2, False, 0, ACT_LEAKY, False),
+    "conv5_res": (32, 64, 128, 128, 64, 3, 1, 1, False, 0, ACT_LEAKY, True),
+    "conv6": (32, 64, 128, 128, 32, 3, 1, 1, False, 0, ACT_LEAKY, False),
     "enhance_64": (32, 208, 64, 64, 208, 3, 1, 1, False, 0, ACT_LEAKY, True),
     "add_64": (32, 80, 64, 64, 80, 5, 1, 2, False, 0, ACT_LEAKY, True),
     "enhance_32": (32, 416, 32, 32, 416, 3, 1, 1, False, 0, ACT_LEAKY, True),

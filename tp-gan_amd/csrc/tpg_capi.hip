@@ -1126,7 +1126,6 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   a.QH = QH; a.QW = QW; a.Cb = d->in_c; a.q_bytes = (int)qb;
   a.kh = d->kh; a.kw = d->kw; a.pt = d->pad_t; a.pl = d->pad_l; a.pad_mode = d->pad_mode;
   a.nr = img ? d->kh : 1;
-  a.nt = img ? d->kw : d->kw == 7 ? 4 : d->kw;
   a.nrg = cdiv(a.kh, a.nr);
   a.tw = img ? tw : 64;
   // tile: fewest padded MACs, the 128 x 64 tile (best operand reuse) on ties
@@ -1143,6 +1142,9 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
       if (best < 0 || cost < best) { best = cost; a.cfg = c; bm = m; bc = b; }
     }
   }
+  // taps per block: a whole kernel row, except 7-wide rows on the 128 x 64 / 256 x 32 tiles
+  // (7 x BC columns there exceed the VGPR budget: 4 + 4 taps, one of them dead)
+  a.nt = img ? d->kw : (d->kw == 7 && (a.cfg == 0 || a.cfg == 6)) ? 4 : d->kw;
   a.nta = cdiv(a.Ca, bm); a.ntb = cdiv(a.Cb, bc);
   a.tiles = a.nta * a.ntb * a.nrg * cdiv(a.kw, a.nt);
   a.nkt = d->n * cdiv(PH, 64 / a.tw) * (PW / a.tw);

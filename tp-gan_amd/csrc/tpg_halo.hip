@@ -48,19 +48,27 @@ typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 __device__ __forceinline__ int hswz(int row) { return ((row >> 2) & 1) << 1; }
 
 __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 128; }
-// epilogue: rows of the 256-row tile parked in LDS per pass (fp32, stride BN + 4); 64 on the
+// epilogue: rows of the tile parked in LDS per pass (fp32, stride BN + 4): 64 on the
 // 192..224-wide tiles, whose waves of the later passes still hold all their accumulators while
-// a pass is finished (128 rows put the 208 / 224 tiles with a producer-x epilogue past 256
-// VGPRs: ~700 B/lane of scratch spills, round 5)
-__host__ __device__ constexpr int halo_epi_rows(int bn) { return bn >= 192 ? 64 : bn >= 80 ? 128 : 256; }
-// (row-offset table [BM][2] int64 + bias [256] floats, then the parked accumulator rows)
-__host__ __device__ constexpr int halo_epi_lds(int bn, int bm = 256) { return bm * 16 + 1024 + halo_epi_rows(bn) * (bn + 4) * 4; }
+// a pass is finished (128 rows put the 224 tile with a producer-x epilogue past 256 VGPRs:
+// scratch spills, round 5); 256 (two passes) on the 512-row tiles
+__host__ __device__ constexpr int halo_epi_rows(int bn, int bm = 256) {
+  return bm == 512 ? 256 : bn >= 192 ? 64 : bn >= 80 ? 128 : 256;
+}
+// the 208-wide tile (8 x 1 waves, 13 fragments per wave) parks column halves instead: every
+// wave its first 7 fragments (112 columns of all rows), then its last 6
+__host__ __device__ constexpr bool halo_epi_colp(int bn) { return bn == 208; }
+__host__ __device__ constexpr int halo_epi_acc_bytes(int bn, int bm = 256) {
+  return halo_epi_colp(bn) ? bm * ((bn / 16 + 1) / 2 * 16 + 4) * 4 : halo_epi_rows(bn, bm) * (bn + 4) * 4;
+}
+// (row-offset table [BM][2] int64 + bias [256] floats, then the parked accumulators)
+__host__ __device__ constexpr int halo_epi_lds(int bn, int bm = 256) { return bm * 16 + 1024 + halo_epi_acc_bytes(bn, bm); }
 // 256-row tiles (all small-map and grouped launches): the row-offset table and the bias live in
 // their own LDS region past both the main loop's buffers (`main` bytes) and the parked rows, so
 // the prologue fills them while its first loads are in flight and the epilogue's residual loads
 // can issue before the accumulators are parked
 __host__ __device__ constexpr int halo_epi_early_off(int main, int bn) {
-  return ((main > halo_epi_rows(bn) * (bn + 4) * 4 ? main : halo_epi_rows(bn) * (bn + 4) * 4) + 15) / 16 * 16;
+  return ((main > halo_epi_acc_bytes(bn) ? main : halo_epi_acc_bytes(bn)) + 15) / 16 * 16;
 }
 
 // mask_chunk on a native 4 x u32 vector (first-class value: stays in VGPRs)
@@ -520,16 +528,32 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   // then every thread finishes 8-channel groups of whole pixel rows: bias, residual and
   // activation with 16-byte residual loads / output stores (or an fp32 partial slice row).
   // Row addresses are computed once per block into a table.
-  constexpr int RP = halo_epi_rows(BN);      // rows per pass (a whole number of wave row-blocks)
-  constexpr int LDW = BN + 4;                // padded fp32 row stride
-  constexpr int CG = BN / 8;                 // 8-channel groups per row
-  constexpr int IPT = (RP * CG + 511) / 512;  // groups per thread per pass (the last partial)
+  // passes: RP rows of all BN columns (the waves owning them park), or for the 208-wide tile
+  // (halo_epi_colp) two column halves in which every wave parks a part of its fragments
+  constexpr bool COLP = halo_epi_colp(BN);
+  static_assert(!COLP || WN == 1, "column passes: one wave column");
+  constexpr int RP = COLP ? BM : halo_epi_rows(BN, BM);  // rows per pass
+  constexpr int NPASS = COLP ? 2 : BM / RP;
+  constexpr int NHP = COLP ? (NREP + 1) / 2 : NREP;       // fragments parked in pass 0
+  constexpr int PW0 = NHP * 16 * (COLP ? 1 : WN), PW1 = COLP ? (NREP - NHP) * 16 : PW0;  // pass columns
+  constexpr int LDW = PW0 + 4;               // padded fp32 row stride
+  constexpr int CG0 = PW0 / 8, CG1 = PW1 / 8;  // 8-channel groups per row of a pass
+  constexpr int IPT = (RP * CG0 + 511) / 512;  // groups per thread per pass (the last partial)
   constexpr int NV = 8 * (int)sizeof(E) / 16;  // 16-byte vectors per group
-  static_assert(RP % WTM == 0, "epilogue tiling");
+  static_assert(RP % WTM == 0 && (COLP || PW0 == BN), "epilogue tiling");
+  static_assert(halo_epi_acc_bytes(BN, BM) == RP * LDW * 4, "epilogue LDS");
   float* s_acc = reinterpret_cast<float*>(lds) + (EARLY ? 0 : BM * 4 + 256);  // [RP][LDW]
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
   const E* XA = reinterpret_cast<const E*>(p.XA);
+  // group it of a pass -> (table row, column in the pass) (compile-time divisors)
+  auto grp = [&](int pass, int it, int& trow, int& c0) __attribute__((always_inline)) {
+    const int cg = (COLP && pass) ? CG1 : CG0;
+    const int row = (COLP && pass) ? it / CG1 : it / CG0;
+    c0 = (it - row * cg) * 8;
+    trow = COLP ? row : pass * RP + row;
+    return row;
+  };
   // residual (or, without one, producer-x) vectors of a pass's groups: bf16 prefetches them,
   // all loads in flight before the first wait; the fp32 parity mode and the rare residual +
   // producer-x case (its x) load in the finishing loop.  One prefetch array: two (round 5's
@@ -541,14 +565,17 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   const bool pvec = pf_r ? p.rvec : p.yvec;
   u32x4 pv[IPT][NV];
   auto prefetch = [&](int pass) __attribute__((always_inline)) {
+    const int ng = RP * ((COLP && pass) ? CG1 : CG0);
+    const int cb = COLP ? pass * PW0 : 0;
 #pragma unroll
     for (int k = 0; k < (PSRC ? PF : 0); ++k) {
-      const int it = min(tid + 512 * k, RP * CG - 1);  // clamped past the last group
-      const int row = it / CG, c0 = (it - row * CG) * 8;
+      int trow, c0;
+      grp(pass, min(tid + 512 * k, ng - 1), trow, c0);  // (clamped past the last group)
       // unconditional (clamped) loads so that all of them issue before the first wait
-      const int64_t yo = s_off[2 * (pass * RP + row)];
-      const bool ok = pvec && p.Nout - (n0 + c0) >= 8 && yo >= 0;
-      const u32x4* src = reinterpret_cast<const u32x4*>(PSRC + (ok ? (pf_r ? s_off[2 * (pass * RP + row) + 1] : yo) + n0 + c0 : 0));
+      const int64_t yo = s_off[2 * trow];
+      const int col = n0 + cb + c0;
+      const bool ok = pvec && p.Nout - col >= 8 && yo >= 0;
+      const u32x4* src = reinterpret_cast<const u32x4*>(PSRC + (ok ? (pf_r ? s_off[2 * trow + 1] : yo) + col : 0));
 #pragma unroll
       for (int v = 0; v < NV; ++v) pv[k][v] = src[v];
     }
@@ -564,9 +591,27 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     __syncthreads();
   }
 #pragma unroll 1
-  for (int pass = 0; pass < BM / RP; ++pass) {
+  for (int pass = 0; pass < NPASS; ++pass) {
     if (!W && (!EARLY || pass > 0)) prefetch(pass);  // (before the park: latency under the park + barrier)
-    if (wm * WTM >= pass * RP && wm * WTM < (pass + 1) * RP) {
+    if constexpr (COLP) {
+      // every wave: fragments [0, NHP) in pass 0, [NHP, NREP) in pass 1 (compile-time indices)
+      float* base = s_acc + (wm * WTM + 4 * g) * LDW + l16;
+      if (pass == 0) {
+#pragma unroll
+        for (int m = 0; m < MREP; ++m)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+            for (int n = 0; n < NHP; ++n) base[(m * 16 + reg) * LDW + n * 16] = acc[m][n][reg];
+      } else {
+#pragma unroll
+        for (int m = 0; m < MREP; ++m)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+            for (int n = NHP; n < NREP; ++n) base[(m * 16 + reg) * LDW + (n - NHP) * 16] = acc[m][n][reg];
+      }
+    } else if (wm * WTM >= pass * RP && wm * WTM < (pass + 1) * RP) {
       float* base = s_acc + (wm * WTM - pass * RP + 4 * g) * LDW + wn * WTN + l16;  // constant offsets below
 #pragma unroll
       for (int m = 0; m < MREP; ++m)
@@ -576,14 +621,17 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
           for (int n = 0; n < NREP; ++n) base[(m * 16 + reg) * LDW + n * 16] = acc[m][n][reg];
     }
     __syncthreads();
+    const int ng = RP * ((COLP && pass) ? CG1 : CG0);
+    const int cb = COLP ? pass * PW0 : 0;  // first tile column of the pass
     if (W) {  // split-K partial slice rows (fp32, row stride Nout)
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const int it = tid + 512 * k;
-        if (it >= RP * CG) continue;  // (compile-time dead unless 512 does not divide RP * CG)
-        const int row = it / CG, c0 = (it - row * CG) * 8;
-        const int64_t yo = s_off[2 * (pass * RP + row)];
-        const int col0 = n0 + c0;
+        if (it >= ng) continue;
+        int trow, c0;
+        const int row = grp(pass, it, trow, c0);
+        const int64_t yo = s_off[2 * trow];
+        const int col0 = n0 + cb + c0;
         const int ncol = min(8, p.Nout - col0);
         if (yo < 0 || ncol <= 0) continue;
         const f32x4 a0 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0);
@@ -602,18 +650,19 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const int it = tid + 512 * k;
-        if (it >= RP * CG) continue;
-        const int row = it / CG, c0 = (it - row * CG) * 8;
-        const int64_t yo = s_off[2 * (pass * RP + row)];
-        const int col0 = n0 + c0;
+        if (it >= ng) continue;
+        int trow, c0;
+        const int row = grp(pass, it, trow, c0);
+        const int64_t yo = s_off[2 * trow];
+        const int col0 = n0 + cb + c0;
         const int ncol = min(8, p.Nout - col0);
         if (yo < 0 || ncol <= 0) continue;
         const f32x4 a0 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0);
         const f32x4 a1 = *reinterpret_cast<const f32x4*>(s_acc + row * LDW + c0 + 4);
         float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
         {
-          const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + c0);
-          const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + c0 + 4);
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cb + c0);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cb + c0 + 4);
 #pragma unroll
           for (int e = 0; e < 4; ++e) { v[e] += b0[e]; v[e + 4] += b1[e]; }
         }
@@ -623,7 +672,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll
           for (int q = 0; q < NV; ++q) rr.u[q] = pv[k][q];
           if (!(full && p.rvec && BF)) {
-            const E* rs = R + s_off[2 * (pass * RP + row) + 1] + col0;
+            const E* rs = R + s_off[2 * trow + 1] + col0;
 #pragma unroll
             for (int e = 0; e < 8; ++e) rr.e[e] = e < ncol ? rs[e] : (E)0.f;
           }
@@ -662,7 +711,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         }
       }
     }
-    if (pass + 1 < BM / RP) __syncthreads();  // before the next pass overwrites s_acc
+    if (pass + 1 < NPASS) __syncthreads();  // before the next pass overwrites s_acc
   }
 #ifdef TPG_BLOCK_TIMING
   __syncthreads();

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   constexpr int PB = (BYTES_B + 1023) / 1024, GB = (PB + 7) / 8;  // X pieces, per wave
   constexpr int RPP = 1024 / RBA, RPB = 1024 / RBB;              // rows per piece
   constexpr int STAGE = BYTES_A + GB * 8 * 1024;
-  static_assert(NR == 1 ? (NT >= 3 && NT <= 5) : (NR == NT && NT <= 3), "taps per block");
+  static_assert(NR == 1 ? ((NT >= 3 && NT <= 5) || NT == 7) : (NR == NT && NT <= 3), "taps per block");
   static_assert(GA * 8192 == BYTES_A && GA >= 1 && GB <= 2, "dma pieces");
   static_assert(MREP * 16 * WM == BM && NREP * 16 * WN == BN, "waves");
 
@@ -467,6 +467,10 @@ static int launch_rh_cfg(const WgradRHArgs& a, hipStream_t s) {
     if (a.nr == 1 && a.nt == 3) return launch_rh_t<1, 3, BM, BC>(a, s);
     if (a.nr == 1 && a.nt == 4) return launch_rh_t<1, 4, BM, BC>(a, s);
     if (a.nr == 1 && a.nt == 5) return launch_rh_t<1, 5, BM, BC>(a, s);
+    // a whole 7-tap kernel row per block (7x7 convs): the 4 + 4 grouping computed a dead tap
+    // column; only the tiles whose 7 x BC columns keep the fragments within the VGPR budget
+    if constexpr (ID >= 1 && ID <= 3)
+      if (a.nr == 1 && a.nt == 7) return launch_rh_t<1, 7, BM, BC>(a, s);
   } else {
     if (a.nr == 2 && a.nt == 2) return launch_rh_t<2, 2, BM, BC>(a, s);
     if (a.nr == 3 && a.nt == 3) return launch_rh_t<3, 3, BM, BC>(a, s);
