@@ -26,7 +26,12 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
 sys.path.insert(0, REPO)
 
-if "--graph" in sys.argv:
+# Launch mode: one process (N = 1) replays the whole step as a hipGraph by default (r05ac, same
+# box: 30.39 / 30.46 vs 31.10 / 30.97 ms/step eager); data-parallel ranks run eager, where each
+# gradient bucket's all-reduce overlaps the rest of the backward (graph replays would issue the
+# whole-network exchange between phase graphs, exposed).  --eager / --graph force either.
+GRAPH_DEFAULT = int(os.environ.get("WORLD_SIZE", "1")) == 1 and "--eager" not in sys.argv
+if "--graph" in sys.argv or GRAPH_DEFAULT:
     # hipGraph replay that keeps the side-stream branches concurrent: without packet capture
     # the runtime launches independent graph branches on up to 8 streams (with it, every node
     # goes to the launch stream in topological order: 39.6 vs 37.0 ms/step).  Read by the HIP
@@ -65,7 +70,9 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as hipGraph(s) with packet capture off and 8 graph queues, so the "
-                         "side-stream branches stay concurrent (37.0 ms/step, no faster than eager: DESIGN.md §4)")
+                         "side-stream branches stay concurrent (the default at N = 1; at N > 1 one graph per "
+                         "phase with the all-reduces between them)")
+    ap.add_argument("--eager", action="store_true", help="launch the step eagerly (the default at N > 1)")
     ap.add_argument("--segmented", action="store_true", help="one hipGraph per step phase even at world 1")
     ap.add_argument("--probe-steps", type=int, default=2)
     ap.add_argument("--identity", choices=["none", "resnet50", "mobilenetv2"], default=None,
@@ -140,10 +147,19 @@ def main():
     if os.environ.get("TPG_TUNE_DUMP") and rank == 0:  # the weight-gradient tiles the autotuner picked
         tpgan_ops.save_tuning(os.environ["TPG_TUNE_DUMP"])
     torch.cuda.synchronize()
-    graphed = args.graph
+    graphed = args.graph or (world == 1 and not args.eager)
     if graphed:
-        trainer.capture(batch, warmup=1, segmented=args.segmented or None)
-        trainer.step_graphed()
+        try:
+            trainer.capture(batch, warmup=1, segmented=args.segmented or None)
+            trainer.step_graphed()
+        except RuntimeError as e:  # (a capture the runtime refuses: the eager step is the same work)
+            if args.graph:
+                raise
+            print("bench: graph capture failed (%s), timing eager steps" % e, file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            trainer._capturing, trainer._graphs = False, []
+            graphed = False
+    if graphed:
         run = trainer.step_graphed
     else:
         def run():
