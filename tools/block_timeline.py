@@ -77,8 +77,9 @@ def run(name, s, passes, dalgo, dsplit, buf, lib):
         torch.cuda.synchronize()
         fn()
         torch.cuda.synchronize()
-        t = buf.view(-1, 4).cpu()
-        t = t[t[:, 0] != 0].double() * 0.01  # 100 MHz ticks -> us
+        t8 = buf.view(-1, 8).cpu()
+        t8 = t8[t8[:, 0] != 0].double() * 0.01  # 100 MHz ticks -> us
+        t = t8[:, :4]
         if t.numel() == 0:
             print("%-10s %-5s no instrumented blocks" % (name, kind), flush=True)
             continue
@@ -95,6 +96,11 @@ def run(name, s, passes, dalgo, dsplit, buf, lib):
               % (name, kind, dalgo, dsplit, call_us, span, t.shape[0], late, pct(start, .5), pct(start, .9),
                  max(start), sum(pro) / len(pro), max(pro), sum(loop) / len(loop), max(loop),
                  sum(epi) / len(epi), max(epi)), flush=True)
+        x = t8[(t8[:, 4] != 0) & (t8[:, 5] != 0) & (t8[:, 6] != 0)]
+        if x.shape[0]:  # halo epilogue: to the table/barrier (4), pass 0 parked (5), pass 0 finished (6)
+            m = lambda a, b: ((x[:, b] - x[:, a]).mean().item())  # noqa: E731
+            print("%-10s %-5s   halo epilogue: start->4 %.1f  4->park0 %.1f  park0->fin0 %.1f  fin0->end %.1f"
+                  % (name, kind, m(2, 4), m(4, 5), m(5, 6), m(6, 3)), flush=True)
 
 
 def main():
@@ -110,7 +116,7 @@ def main():
         raise SystemExit("needs the -DTPG_BLOCK_TIMING ablation build (TPG_LIB_PATH)")
     if a.tune_file:
         T.load_tuning(a.tune_file)
-    buf = torch.zeros(CAP * 4, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(CAP * 8, dtype=torch.int64, device="cuda")
     for f in [getattr(lib, n) for n in ("tpg_abl_tl_pw", "tpg_abl_tl_halo", "tpg_abl_tl_wgrad2") if hasattr(lib, n)]:
         f.argtypes = [ctypes.c_void_p]
         assert f(buf.data_ptr()) == 0

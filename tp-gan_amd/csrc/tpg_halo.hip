@@ -113,6 +113,9 @@ __device__ __forceinline__ u32x4 act_mask_chunk(u32x4 g, u32x4 y, int act, float
 
 TPG_TL_DEFINE(halo)
 
+// workgroup barrier for LDS hand-offs only (no vmcnt drain: vector loads stay in flight)
+#define EPI_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
 template <int DT, int HL, int BN, int WM, int WN, bool MASK, int BM = 256, int NG = 1>
 __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> GA) {
   TPG_TL_MARK(0);
@@ -585,11 +588,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     // the halo / ring space for the parked rows)
     if (!W) prefetch(0);
   }
-  __syncthreads();                           // every wave is done with the halo and the ring
+  // (epilogue barriers wait for LDS only: __syncthreads() would also drain vmcnt, i.e. wait for
+  // the residual / producer-x loads prefetched just before it -- 2-4 us per pass measured)
+  EPI_BARRIER();                             // every wave is done with the halo and the ring
   if constexpr (!EARLY) {
     epi_table();
-    __syncthreads();
+    EPI_BARRIER();
   }
+  TPG_TL_MARK(4);
 #pragma unroll 1
   for (int pass = 0; pass < NPASS; ++pass) {
     if (!W && (!EARLY || pass > 0)) prefetch(pass);  // (before the park: latency under the park + barrier)
@@ -620,7 +626,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll
           for (int n = 0; n < NREP; ++n) base[(m * 16 + reg) * LDW + n * 16] = acc[m][n][reg];
     }
-    __syncthreads();
+    EPI_BARRIER();
+    if (pass == 0) TPG_TL_MARK(5);
     const int ng = RP * ((COLP && pass) ? CG1 : CG0);
     const int cb = COLP ? pass * PW0 : 0;  // first tile column of the pass
     if (W) {  // split-K partial slice rows (fp32, row stride Nout)
@@ -711,7 +718,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
         }
       }
     }
-    if (pass + 1 < NPASS) __syncthreads();  // before the next pass overwrites s_acc
+    if (pass + 1 < NPASS) EPI_BARRIER();  // before the next pass overwrites s_acc
+    if (pass == 0) TPG_TL_MARK(6);
   }
 #ifdef TPG_BLOCK_TIMING
   __syncthreads();

@@ -100,8 +100,8 @@ struct FastDiv {
 // DMA'd bytes themselves (s_waitcnt vmcnt + s_barrier); the pass, not seeing these loads, only
 // ever waits for more VMEM operations than it needs (in-order completion), never fewer.
 // Per-block timeline (ablation builds only, -DTPG_BLOCK_TIMING; tools/block_timeline.py): thread 0
-// of every block stores s_memrealtime (100 MHz) at kernel entry, before the main loop, after it
-// and at the end, into the buffer a per-file tpg_abl_tl_<file>() set (vector stores).
+// of every block stores s_memrealtime (100 MHz) at kernel entry (0), before the main loop (1), after
+// it (2) and at the end (3), plus kernel-specific marks 4..7, into the buffer a per-file tpg_abl_tl_<file>() set (vector stores).
 #ifdef TPG_BLOCK_TIMING
 #define TPG_TL_DEFINE(NAME)                                                                    \
   __device__ unsigned long long* g_tl_buf = nullptr;                                          \
@@ -112,7 +112,7 @@ struct FastDiv {
   do {                                                                                         \
     unsigned long long* b_ = g_tl_buf;                                                         \
     if (b_ && threadIdx.x == 0)                                                                \
-      b_[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + (i)] =         \
+      b_[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + (i)] =         \
           __builtin_amdgcn_s_memrealtime();                                                    \
   } while (0)
 #else
