@@ -303,6 +303,35 @@ def test_graph_replay_segmented_with_identity(gpu):
             assert np.isfinite(a) and abs(a - c) <= 1e-6 * max(abs(c), 1e-3), (s, k, a, c)
 
 
+def test_identity_side_stream_bit_identical(gpu):
+    """tpgan_train.IDENTITY_STREAM: the identity loss (and, through autograd's stream rule, its
+    input-gradient backward) on a side stream beside D(fake) gives the same step as one stream
+    (bf16, deterministic: the same kernels in the same order per stream -> bit-identical)."""
+    import FeatureExtract as FE
+    import tpgan_ops
+    import tpgan_train
+    prev = tpgan_train.IDENTITY_STREAM["enabled"]
+    res = {}
+    try:
+        with tpgan_ops.deterministic():
+            for on in (False, True):
+                tpgan_train.IDENTITY_STREAM["enabled"] = on
+                G, D = _models(gpu)
+                torch.manual_seed(0)
+                ext = FE.FeatureExtractModel("resnet50", 347).to(gpu)
+                tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16,
+                                              use_dropout=False,
+                                              identity_fn=FE.IdentityPreservingLoss(ext, torch.bfloat16))
+                b = tpgan_train.synthetic_batch(2, gpu, seed=17)
+                outs = [tr.step(b) for _ in range(2)]
+                torch.cuda.synchronize()
+                res[on] = (tr.fG.data.clone(), tr.fD.data.clone(), [float(o["loss_G"]) for o in outs])
+    finally:
+        tpgan_train.IDENTITY_STREAM["enabled"] = prev
+    assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
+    assert res[True][2] == res[False][2]
+
+
 def test_gradient_penalty_double_backward_vs_oracle(gpu):
     """WGAN-GP through the HIP double backward: the penalty and D's parameter gradients
     of it against torch's double backward of the oracle D (float64 CPU), global 1e-3."""

@@ -1,7 +1,7 @@
 """bench.py with tpgan_ops module switches set first (for same-box kernel-trace A/Bs under
 rocprofv3, which must launch python3 on a script directly):
 
-    python tools/bench_variant.py CAT_LINK=0 ACT_LINK=1 -- --steps 10 --warmup 5 --no-cpu-baseline
+    python tools/bench_variant.py CAT_LINK=0 tpgan_train.IDENTITY_STREAM=0 -- --steps 10 --no-cpu-baseline
 """
 import os
 import sys
@@ -14,10 +14,11 @@ def main():
     argv = sys.argv[1:]
     sets = argv[:argv.index("--")] if "--" in argv else argv
     rest = argv[argv.index("--") + 1:] if "--" in argv else []
-    import tpgan_ops
-    for kv in sets:
+    import importlib
+    for kv in sets:  # SWITCH=v (a tpgan_ops switch) or module.SWITCH=v (e.g. tpgan_train.IDENTITY_STREAM=0)
         k, v = kv.split("=")
-        getattr(tpgan_ops, k)["enabled"] = bool(int(v))
+        mod, _, name = k.rpartition(".")
+        getattr(importlib.import_module(mod or "tpgan_ops"), name)["enabled"] = bool(int(v))
     sys.argv = [os.path.join(REPO, "bench.py")] + rest
     import bench
     bench.main()

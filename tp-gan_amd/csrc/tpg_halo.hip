@@ -55,9 +55,15 @@ __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 1
 __host__ __device__ constexpr int halo_epi_rows(int bn, int bm = 256) {
   return bm == 512 ? 256 : bn >= 192 ? 64 : bn >= 80 ? 128 : 256;
 }
-// the 208-wide tile (8 x 1 waves, 13 fragments per wave) parks column halves instead: every
-// wave its first 7 fragments (112 columns of all rows), then its last 6
-__host__ __device__ constexpr bool halo_epi_colp(int bn) { return bn == 208; }
+// Column-half passes for the 208-wide tile (8 x 1 waves, 13 fragments per wave: every wave
+// parks its first 7 fragments, then its last 6) -- built and measured, not used: 1.5 % faster
+// per enhance_128 launch than four 64-row passes, but every 416-byte pixel row is then written
+// (and its residual read) in two passes, so the 128-byte lines at the split are touched twice:
+// HBM traffic 895 -> 990 MB per launch (1.36x -> 1.51x algorithmic, gpurun r05ao PMC)
+#ifndef TPG_HALO_COLP
+#define TPG_HALO_COLP 0
+#endif
+__host__ __device__ constexpr bool halo_epi_colp(int bn) { return TPG_HALO_COLP && bn == 208; }
 __host__ __device__ constexpr int halo_epi_acc_bytes(int bn, int bm = 256) {
   return halo_epi_colp(bn) ? bm * ((bn / 16 + 1) / 2 * 16 + 4) * 4 : halo_epi_rows(bn, bm) * (bn + 4) * 4;
 }

@@ -454,6 +454,16 @@ TUNE_UNGROUPED = {"enabled": True}
 # (tpgan_ops.image_losses / l1_means); False: the aten expressions (A/B, tests)
 FUSED_LOSSES = {"enabled": True}
 
+# the identity-preserving loss (configs[2] / [4]: a frozen ResNet-50 / MobileNetV2 on the fake
+# face) on a side stream of its own, beside D's Adam, the frozen D(fake) and the other G losses;
+# its input-gradient backward then runs on that stream too (autograd replays each node on its
+# forward's stream), beside D(fake)'s.  Both paths are chains of small-map layers that leave
+# most of the chip idle: configs[2] eager 38.19 / 37.95 -> 34.50 / 35.41 ms/step (gpurun r05ak).
+# Off by default: a process that ran eager steps with this fork and then captured the step as a
+# hipGraph crashed in the first replay (gpurun r05aj / r05ak / r05al; without the fork the same
+# capture replays fine, r05am) -- not yet understood.  bench.py turns it on for eager runs only.
+IDENTITY_STREAM = {"enabled": False}
+
 
 def total_variation(x):
     return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
@@ -524,6 +534,7 @@ class TPGANTrainer:
         self.real_ahead_used = 0  # steps whose D(real) came from the previous step's real_ahead pass
         self._capturing = False
         self._segmented = False
+        self._graph_setup = False  # (inside capture(), warm-up steps included)
         self.comm_timing = False  # exposed-communication events around each exchange (exposed_comm_ms)
         self.comm_events = []
         self.identity_fn = identity_fn
@@ -682,6 +693,22 @@ class TPGANTrainer:
         w = self.w
         D = self.D
         fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = self._st.pop("outs")
+        front = b["frontal"]
+        id_st, l_ip = None, None
+        # (eager training only: not in capture() -- its warm-up steps included -- since bench runs
+        # with this fork in the warm-up of a whole-step capture crashed the process, gpurun r05aj /
+        # r05ak, not yet understood; the captured step keeps the one-stream identity pass)
+        if (self.identity_fn is not None and IDENTITY_STREAM["enabled"] and fake.is_cuda and
+                tpgan_ops.MULTISTREAM and not self._capturing and not self._graph_setup):
+            main = torch.cuda.current_stream()
+            id_st = tpgan_ops.side_streams(fake.device, 1, "identity-fake")[0]
+            id_st.wait_stream(main)
+            with torch.cuda.stream(id_st):
+                l_ip = self._identity_loss(fake, front)
+        elif self.identity_fn is not None:
+            # (the same point of the autograd graph as the side-stream form: the gradients at
+            # `fake` are then summed in the same order, and the two forms are bit-identical)
+            l_ip = self._identity_loss(fake, front)
         with tpgan_ops.compute_dtype(self.dtype):
             self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
                          check_finite=self.loss_scale != 1.0)
@@ -689,17 +716,14 @@ class TPGANTrainer:
             set_requires_grad(D.parameters(), False)
             d_gen = D(fake).float()
             set_requires_grad(D.parameters(), True)
-        front = b["frontal"]
         args = (fake, le_f, re_f, no_f, mo_f, d_gen, pred, front, b["frontal_left_eye"], b["frontal_right_eye"],
                 b["frontal_nose"], b["frontal_mouth"], b["label"])
         loss_G = self._g_losses(*args)
-        f32 = fake.float() if self.identity_fn is not None else None
         if self.identity_fn is not None:
-            if self._id_pre is not None:
-                l_ip = self.identity_fn(f32, front, pre=self._id_pre)
-                self._id_pre = None
-            else:
-                l_ip = self.identity_fn(f32, front)
+            if id_st is not None:
+                main = torch.cuda.current_stream()
+                main.wait_stream(id_st)
+                l_ip.record_stream(main)
             loss_G = loss_G + w["weight_identity_preserving"] * l_ip
         if self.gsync is not None and not self._capturing:
             if self.gsync.optimizer is not None:
@@ -708,6 +732,13 @@ class TPGANTrainer:
         with tpgan_ops.roctx_range("G-bwd"), tpgan_ops.wgrad_side_stream():
             (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
         self._st["loss_G"] = loss_G.detach()
+
+    def _identity_loss(self, fake, front):
+        f32 = fake.float()
+        if self._id_pre is not None:
+            pre, self._id_pre = self._id_pre, None
+            return self.identity_fn(f32, front, pre=pre)
+        return self.identity_fn(f32, front)
 
     def _g_losses(self, fake, le_f, re_f, no_f, mo_f, d_gen, pred, front, fle, fre, fno, fmo, label):
         """The G-step's pixel, local, symmetry, adversarial, total-variation and identity-class
@@ -870,6 +901,13 @@ class TPGANTrainer:
         step_graphed() copies new data into it.  Warm-up steps (which also run the
         weight-gradient autotuner, and train the model) run on a side stream first, as
         capture requires."""
+        self._graph_setup = True
+        try:
+            self._capture(b, warmup, segmented)
+        finally:
+            self._graph_setup = False
+
+    def _capture(self, b, warmup, segmented):
         self._static = {k: v.clone() for k, v in b.items()}
         self._d_real_next = None  # (graph replays never run the eager real_ahead pass)
         gc.collect()  # (nothing of earlier steps or trainers may be freed while a graph is being captured)
