@@ -108,12 +108,6 @@ def main():
         else:
             dist.init_process_group("gloo")
     torch.manual_seed(1234)
-    # eager steps run the identity loss (configs[2] / [4]) on a side stream beside D(fake)
-    # (configs[2] eager: 38.19 / 37.95 -> 34.50 / 35.41 ms/step, gpurun r05ak); a process that
-    # will capture the step keeps it on one stream (tpgan_train.IDENTITY_STREAM)
-    import tpgan_train
-    tpgan_train.IDENTITY_STREAM["enabled"] = not (args.graph or (world == 1 and not args.eager))
-
     import D_and_G_model as DG
     import tpgan_ops
     import tpgan_train

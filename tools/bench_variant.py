@@ -15,10 +15,11 @@ def main():
     sets = argv[:argv.index("--")] if "--" in argv else argv
     rest = argv[argv.index("--") + 1:] if "--" in argv else []
     import importlib
-    for kv in sets:  # SWITCH=v (a tpgan_ops switch) or module.SWITCH=v (e.g. tpgan_train.IDENTITY_STREAM=0)
+    for kv in sets:  # SWITCH=v (a tpgan_ops switch), module.SWITCH=v or module.SWITCH:key=v
         k, v = kv.split("=")
+        k, _, key = k.partition(":")
         mod, _, name = k.rpartition(".")
-        getattr(importlib.import_module(mod or "tpgan_ops"), name)["enabled"] = bool(int(v))
+        getattr(importlib.import_module(mod or "tpgan_ops"), name)[key or "enabled"] = bool(int(v))
     sys.argv = [os.path.join(REPO, "bench.py")] + rest
     import bench
     bench.main()

@@ -455,14 +455,15 @@ TUNE_UNGROUPED = {"enabled": True}
 FUSED_LOSSES = {"enabled": True}
 
 # the identity-preserving loss (configs[2] / [4]: a frozen ResNet-50 / MobileNetV2 on the fake
-# face) on a side stream of its own, beside D's Adam, the frozen D(fake) and the other G losses;
-# its input-gradient backward then runs on that stream too (autograd replays each node on its
+# face) on a side stream, beside D's Adam, the frozen D(fake) and the other G losses; its
+# input-gradient backward then runs on that stream too (autograd replays each node on its
 # forward's stream), beside D(fake)'s.  Both paths are chains of small-map layers that leave
 # most of the chip idle: configs[2] eager 38.19 / 37.95 -> 34.50 / 35.41 ms/step (gpurun r05ak).
-# Off by default: a process that ran eager steps with this fork and then captured the step as a
-# hipGraph crashed in the first replay (gpurun r05aj / r05ak / r05al; without the fork the same
-# capture replays fine, r05am) -- not yet understood.  bench.py turns it on for eager runs only.
-IDENTITY_STREAM = {"enabled": False}
+# The stream is the real-image features' one (they ran in phase A): a process holding one more
+# stream crashed in the first replay of a later whole-step capture (r05aj-r05al; reusing the
+# stream, r05aq, it does not).  Not inside capture() ("in_capture"): hipStreamEndCapture
+# crashed with the fork in the graph (r05ar).  False: everything on the step's stream.
+IDENTITY_STREAM = {"enabled": True, "in_capture": False}
 
 
 def total_variation(x):
@@ -699,9 +700,11 @@ class TPGANTrainer:
         # with this fork in the warm-up of a whole-step capture crashed the process, gpurun r05aj /
         # r05ak, not yet understood; the captured step keeps the one-stream identity pass)
         if (self.identity_fn is not None and IDENTITY_STREAM["enabled"] and fake.is_cuda and
-                tpgan_ops.MULTISTREAM and not self._capturing and not self._graph_setup):
+                tpgan_ops.MULTISTREAM and
+                (not self._graph_setup or IDENTITY_STREAM.get("in_capture", False))):
             main = torch.cuda.current_stream()
-            id_st = tpgan_ops.side_streams(fake.device, 1, "identity-fake")[0]
+            # (the real-image features' stream: they ran in phase A, so the two never overlap)
+            id_st = tpgan_ops.side_streams(fake.device, 1, "identity")[0]
             id_st.wait_stream(main)
             with torch.cuda.stream(id_st):
                 l_ip = self._identity_loss(fake, front)
