@@ -19,7 +19,8 @@ def main():
         k, v = kv.split("=")
         k, _, key = k.partition(":")
         mod, _, name = k.rpartition(".")
-        getattr(importlib.import_module(mod or "tpgan_ops"), name)[key or "enabled"] = bool(int(v))
+        getattr(importlib.import_module(mod or "tpgan_ops"), name)[key or "enabled"] = (
+            float(v) if "." in v else bool(int(v)))
     sys.argv = [os.path.join(REPO, "bench.py")] + rest
     import bench
     bench.main()
