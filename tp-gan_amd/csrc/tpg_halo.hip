@@ -458,8 +458,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   //                retires step s+1's DMA (issued during s-1) while step s+2's stays in
   //                flight; lgkmcnt(0); s_barrier.  Step s+1 then reads what was retired.
   // epilogue row table: output / residual element offsets of each of the BM rows (-1 = no row),
-  // or the split-K slice row; and the bias of this block's columns
+  // or the split-K slice row; and the bias of this block's columns, loaded into a register
+  // here (the 512-row tiles fill their table after the loop, where the load's latency showed)
   float* W = p.ws ? p.ws + (int64_t)z * p.N * p.JH * p.JW * p.Nout : nullptr;
+  float bias_pre = 0.f;
+  if (tid >= 512 - BN) {
+    const int c = n0 + tid - (512 - BN);
+    if (p.bias && c < p.Nout) bias_pre = p.bias[c];
+  }
   auto epi_table = [&]() {
     for (int q = tid; q < BM; q += 512) {
       const int sub = (int)p.fd_thw.div(q), rem = q - sub * THW;
@@ -483,10 +489,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       s_off[2 * q] = yo;
       s_off[2 * q + 1] = ro;
     }
-    if (tid >= 512 - BN) {  // (the highest threads: BM >= 256 > BN)
-      const int c = n0 + tid - (512 - BN);
-      s_bias[tid - (512 - BN)] = (p.bias && c < p.Nout) ? p.bias[c] : 0.f;
-    }
+    if (tid >= 512 - BN) s_bias[tid - (512 - BN)] = bias_pre;  // (the highest threads: BM >= 256 > BN)
   };
 
   const int ntaps = p.ntaps;
