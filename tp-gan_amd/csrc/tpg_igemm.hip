@@ -294,16 +294,37 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
     int j = rem / p.JW, i = rem - j * p.JW;
     int oy = p.oy0 + p.osy * j, ox = p.ox0 + p.osx * i;
     float v[V];
+    // slices summed in order z = 0, 1, ... (deterministic), their loads issued four at a time:
+    // one at a time, every slice exposed a full memory latency (a k split of 8 -> ~8 of them)
     if constexpr (V == 4) {
-      float4 a = *reinterpret_cast<const float4*>(p.ws + e0);
-      for (int z = 1; z < p.nslices; ++z) {
-        const float4 b = *reinterpret_cast<const float4*>(p.ws + z * p.slice + e0);
+      const float* src = p.ws + e0;
+      float4 a = *reinterpret_cast<const float4*>(src);
+      int z = 1;
+      for (; z + 3 < p.nslices; z += 4) {
+        float4 b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(src + (z + u) * p.slice);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w; }
+      }
+      for (; z < p.nslices; ++z) {
+        const float4 b = *reinterpret_cast<const float4*>(src + z * p.slice);
         a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
       }
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     } else {
-      v[0] = p.ws[e0];
-      for (int z = 1; z < p.nslices; ++z) v[0] += p.ws[z * p.slice + e0];
+      const float* src = p.ws + e0;
+      float a = src[0];
+      int z = 1;
+      for (; z + 3 < p.nslices; z += 4) {
+        float b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = src[(z + u) * p.slice];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a += b[u];
+      }
+      for (; z < p.nslices; ++z) a += src[z * p.slice];
+      v[0] = a;
     }
     const int64_t yo = (int64_t)n * p.y_sn + (int64_t)oy * p.y_sh + (int64_t)ox * p.y_sw + col;
     const int64_t ro = (int64_t)n * p.r_sn + (int64_t)oy * p.r_sh + (int64_t)ox * p.r_sw + col;
