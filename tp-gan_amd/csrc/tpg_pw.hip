@@ -148,6 +148,8 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the bias of this block's columns, loaded now (its latency under the main loop)
+  const float bias_pre = (tid < BN && p.bias && n0 + tid < p.Nout) ? p.bias[n0 + tid] : 0.f;
   __syncthreads();  // (tap table)
   TPG_TL_MARK(1);
   if (total > 0) {
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
     s_off[2 * q] = yo;
     s_off[2 * q + 1] = ro;
   }
-  for (int c = tid; c < BN; c += 256) s_bias[c] = (p.bias && n0 + c < p.Nout) ? p.bias[n0 + c] : 0.f;
+  if (tid < BN) s_bias[tid] = bias_pre;
   {
     float* base = s_acc + (wm * WTM + 4 * g) * LDW + wn * WTN + l16;
 #pragma unroll
@@ -235,7 +237,29 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
   E* Y = reinterpret_cast<E*>(p.Y);
   const E* R = reinterpret_cast<const E*>(p.R);
   const E* XA = reinterpret_cast<const E*>(p.XA);
-  for (int it = tid; it < BM * CG; it += 256) {
+  // groups it = tid + 256 k: the residual (or, without one, the producer's x) of every group is
+  // loaded first -- one memory latency per thread instead of one per group
+  constexpr int IT = BM * CG / 256;
+  static_assert(IT * 256 == BM * CG, "whole groups per thread");
+  const bool pf_r = R != nullptr;
+  const E* PSRC = pf_r ? R : XA;
+  const bool pvec = pf_r ? p.rvec : p.yvec;
+  u32x4 pv[IT][NV];
+  if (!Wsk && PSRC) {
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int it = tid + 256 * k;
+      const int row = it / CG, c0 = (it - row * CG) * 8;
+      const int64_t yo = s_off[2 * row];
+      const bool ok = pvec && p.Nout - (n0 + c0) >= 8 && yo >= 0;
+      const u32x4* src = reinterpret_cast<const u32x4*>(PSRC + (ok ? (pf_r ? s_off[2 * row + 1] : yo) + n0 + c0 : 0));
+#pragma unroll
+      for (int q = 0; q < NV; ++q) pv[k][q] = src[q];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int it = tid + 256 * k;
     const int row = it / CG, c0 = (it - row * CG) * 8;
     const int64_t yo = s_off[2 * row];
     const int col0 = n0 + c0;
@@ -261,11 +285,10 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
     const bool full = ncol == 8;
     if (R) {
       union { u32x4 u[NV]; E e[8]; } rr;
-      const E* rs = R + s_off[2 * row + 1] + col0;
-      if (full && p.rvec) {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) rr.u[q] = reinterpret_cast<const u32x4*>(rs)[q];
-      } else {
+      for (int q = 0; q < NV; ++q) rr.u[q] = pv[k][q];
+      if (!(full && p.rvec)) {
+        const E* rs = R + s_off[2 * row + 1] + col0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) rr.e[e] = e < ncol ? rs[e] : (E)0.f;
       }
@@ -275,11 +298,14 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
     union { u32x4 u[NV]; E e[8]; } o;
     if (XA) {  // desc.in_act: v * xa_act'(x), x at the output's offsets
       union { u32x4 u[NV]; E e[8]; } xx;
-      const E* xs = XA + yo + col0;
-      if (full && p.yvec) {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) xx.u[q] = reinterpret_cast<const u32x4*>(xs)[q];
-      } else {
+      for (int q = 0; q < NV; ++q) xx.u[q] = pv[k][q];
+      if (pf_r && full && p.yvec) {  // (residual prefetched: x loaded here)
+        const u32x4* xs = reinterpret_cast<const u32x4*>(XA + yo + col0);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) xx.u[q] = xs[q];
+      } else if (!(full && p.yvec)) {
+        const E* xs = XA + yo + col0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) xx.e[e] = e < ncol ? xs[e] : (E)0.f;
       }
