@@ -4,6 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` (N > 1) without a launcher starts the second form itself, as a child process, and
+exits with its code; under a launcher every rank checks that --gpus equals WORLD_SIZE, and
+with nccl that the node has a GPU per local rank.
+
 Workload = BASELINE.json configs[1]: full two-pathway Generator (global + 4 local
 pathways) + Discriminator train step, 128x128, bs32 per GPU, bf16 activations / MFMA
 with fp32 accumulate and fp32 master weights, synthetic Multi-PIE-shaped data resident in
@@ -25,6 +29,47 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "tp-gan_amd"))
 sys.path.insert(0, REPO)
+
+
+def argv_gpus(argv):
+    """The --gpus value of a command line, read before argparse (and before torch is imported);
+    None when absent."""
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return None
+
+
+def launcher_cmd(argv, n, port):
+    """The torch.distributed.run command that starts n ranks of this script, one per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv):
+    """`bench.py --gpus N` (N > 1) with no launcher in front: start N ranks under
+    torch.distributed.run as a CHILD process (never an exec -- nothing here has touched the GPU or
+    imported torch), pass its output through (rank 0 prints the JSON line) and return its exit
+    code.  None when this process is itself a rank (WORLD_SIZE set) or N <= 1."""
+    n = argv_gpus(argv)
+    if n is None or n <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(launcher_cmd(argv, n, port), env=env)
+
+
+if __name__ == "__main__":
+    _rc = launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
 
 # Launch mode: one process (N = 1) replays the whole step as a hipGraph by default (r05ac, same
 # box: 30.39 / 30.46 vs 31.10 / 30.97 ms/step eager); data-parallel ranks run eager, where each
@@ -53,7 +98,9 @@ PASS_KERNEL = {"fwd": "halo_kernel forward",
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (one process each).  N > 1 without a launcher: bench.py starts "
+                         "torch.distributed.run itself; under a launcher it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, choices=[2, 3, 5], default=2,
@@ -96,10 +143,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; ranks beyond the visible devices share them (the gloo rehearsal of
-    # this path runs two ranks on one GPU -- RCCL itself needs a device per rank)
+    # the JSON line's n_gpus is the world size: a --gpus that disagrees with the ranks actually
+    # started would misreport, so it is an error (checked before anything touches the GPU)
+    if args.gpus is not None and args.gpus != world:
+        sys.exit("bench.py: --gpus %d but this run has %d rank(s) (WORLD_SIZE=%s)"
+                 % (args.gpus, world, os.environ.get("WORLD_SIZE", "unset")))
+    # one process per GPU.  RCCL needs a device per rank: with nccl, fewer devices than local
+    # ranks is an error; only the gloo rehearsal of this path (two ranks on one GPU,
+    # tests/test_gpu_bench_dp.py) shares a device
     # (device_count does not initialise HIP: nothing GPU-side happens before the process group)
-    ndev = max(torch.cuda.device_count(), 1)
+    ndev_seen = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > 1 and args.dist_backend == "nccl" and ndev_seen < local_world:
+        sys.exit("bench.py: rank %d: %d ranks on this node but %d visible GPU(s); RCCL needs one device per rank"
+                 % (rank, local_world, ndev_seen))
+    ndev = max(ndev_seen, 1)
     dev = torch.device("cuda", local % ndev)
     if world > 1:
         torch.cuda.set_device(dev)
@@ -147,6 +205,7 @@ def main():
         tpgan_ops.save_tuning(os.environ["TPG_TUNE_DUMP"])
     torch.cuda.synchronize()
     graphed = args.graph or (world == 1 and not args.eager)
+    capture_error = None
     if graphed:
         try:
             trainer.capture(batch, warmup=1, segmented=args.segmented or None)
@@ -154,9 +213,11 @@ def main():
         except RuntimeError as e:  # (a capture the runtime refuses: the eager step is the same work)
             if args.graph:
                 raise
+            # reported in the JSON line (config.capture_error), so a capture regression is visible
+            capture_error = "%s: %s" % (type(e).__name__, str(e)[:400])
             print("bench: graph capture failed (%s), timing eager steps" % e, file=sys.stderr, flush=True)
             torch.cuda.synchronize()
-            trainer._capturing, trainer._graphs = False, []
+            trainer.reset_capture()
             graphed = False
     if graphed:
         run = trainer.step_graphed
@@ -303,8 +364,9 @@ def main():
         "data": "synthetic (U[-1,1] Multi-PIE-shaped batch resident in HBM; random-init weights)",
         "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B,
                    "parallelism": "dp%d" % world,
-                   "launch": "eager" if not graphed else ("hipGraph x3 (per phase)" if (world > 1 or args.segmented)
-                                                          else "hipGraph (whole step)")},
+                   "launch": ("eager" + (" (graph capture failed)" if capture_error else "")) if not graphed
+                   else ("hipGraph x3 (per phase)" if (world > 1 or args.segmented) else "hipGraph (whole step)"),
+                   "capture_error": capture_error},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,

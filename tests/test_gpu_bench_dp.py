@@ -27,13 +27,32 @@ def _free_port():
     return p
 
 
+ARGS = ["--gpus", "2", "--steps", "2", "--warmup", "2", "--batch", "2", "--no-cpu-baseline", "--dist-backend", "gloo"]
+
+
+def _rank_env():
+    return {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+
+
+@pytest.mark.timeout(400)
+def test_bench_gpus_flag_alone_launches_two_ranks(gpu):
+    """the driver's command shape, `bench.py --gpus N` with no launcher in
+    front, must run N ranks (bench.py starts torch.distributed.run as its child)."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + ARGS, cwd=REPO, env=_rank_env(),
+                       capture_output=True, text=True, timeout=380)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["dp"]["backend"] == "gloo" and out["value"] > 0
+
+
 @pytest.mark.timeout(400)
 def test_bench_torchrun_two_ranks_one_gpu(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "2", "--batch", "2", "--no-cpu-baseline",
-           "--dist-backend", "gloo"]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py")] + ARGS
+    env = dict(_rank_env(), MASTER_ADDR="127.0.0.1")
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=380)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

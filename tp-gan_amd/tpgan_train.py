@@ -535,6 +535,7 @@ class TPGANTrainer:
         self.real_ahead_used = 0  # steps whose D(real) came from the previous step's real_ahead pass
         self._capturing = False
         self._segmented = False
+        self._graphs = []
         self._graph_setup = False  # (inside capture(), warm-up steps included)
         self.comm_timing = False  # exposed-communication events around each exchange (exposed_comm_ms)
         self.comm_events = []
@@ -970,11 +971,29 @@ class TPGANTrainer:
         self._graph_layout = (self.fG.layout_version, self.fD.layout_version)
         torch.cuda.synchronize()
 
+    def reset_capture(self):
+        """Drop every graph and the state a (possibly failed) capture() left: the graphs and
+        their memory pool, the static batch, the graph outputs; eager step() is then the only
+        launch mode, as before capture()."""
+        self._capturing = False
+        self._segmented = False
+        self._graph_setup = False
+        self._graphs = []
+        self._static = None
+        self._graph_out = None
+        self._graph_layout = None
+        self._st = {}
+        self._id_pre = None
+        gc.collect()
+        torch.cuda.synchronize()
+
     def step_graphed(self, b=None):
         """One train step by graph replay (capture() first).  Returns the step's losses as
         fresh tensors: the graph's own outputs live in its memory pool and the next replay
         overwrites them, so a caller holding step k's dict would otherwise read step k+1's
         values (round 2's graphed-loss experiment returned such aliased outputs)."""
+        if not self._graphs:
+            raise RuntimeError("step_graphed() without a captured step: capture() first")
         if (self.fG.layout_version, self.fD.layout_version) != self._graph_layout:
             raise RuntimeError("the parameters were re-laid out after capture(): the graphs hold the old buffers; "
                                "capture() again")
