@@ -59,9 +59,7 @@ extern "C" {
 typedef void* tpg_stream_t; /* hipStream_t */
 
 enum { TPG_F32 = 0, TPG_BF16 = 1, TPG_F16 = 2 };
-enum { TPG_ACT_NONE = 0, TPG_ACT_RELU = 1, TPG_ACT_LEAKY = 2, TPG_ACT_RELU6 = 3, TPG_ACT_CHANNEL = 4 };
-/* TPG_ACT_CHANNEL: desc.in_act only -- a slope per channel segment, act'(x) = x > 0 ? 1 : slope (LeakyReLU
-   slope, 0 for ReLU, 1 for no activation): the channel slices of a concat of differently activated layers */
+enum { TPG_ACT_NONE = 0, TPG_ACT_RELU = 1, TPG_ACT_LEAKY = 2, TPG_ACT_RELU6 = 3 };
 enum { TPG_PAD_ZERO = 0, TPG_PAD_REFLECT = 1 };
 enum { TPG_OP_FWD = 0, TPG_OP_BWD_DATA = 1, TPG_OP_BWD_FILTER = 2 };
 
@@ -112,10 +110,6 @@ typedef struct tpg_conv_desc {
                                      DX_ACCUM add), so the producer's own backward takes it as its
                                      already-masked g.  0 (TPG_ACT_NONE) everywhere else */
   float in_slope;                 /* LeakyReLU negative slope of in_act */
-  int32_t in_nseg;                /* in_act == TPG_ACT_CHANNEL: channel c takes the slope of the first of the
-                                     in_nseg (1..4) segments with c < in_seg_end[k] */
-  int32_t in_seg_end[4];
-  float in_seg_slope[4];
 } tpg_conv_desc;
 
 enum { TPG_FLAG_WPACKED = 1, TPG_FLAG_CONCURRENT = 2, TPG_FLAG_DX_ACCUM = 4 };
@@ -232,30 +226,6 @@ int32_t tpg_maxout2_bwd(int32_t b, int32_t m, tpg_tensor gy, const uint8_t* argm
 int32_t tpg_adam(int64_t numel, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  float grad_scale, float* state, tpg_stream_t stream);
-
-/* Adam fused with the repack of the weights' pre-packed images (one launch instead of tpg_adam +
- * tpg_pack_run over the owner images; UtilityMethods.py:14-41 getOptimizer 'Adam' + the
- * packing of tpg_conv2d_pack_jobs):
- *   tpg_adam_pack_owner_ok  1 when the pack job `job` (one of tpg_conv2d_pack_jobs' jobs) packs
- *                           every one of a parameter's numel elements exactly once with unit
- *                           channel stride (it may then OWN the parameter's update), else 0
- *   tpg_adam_pack_jobs      lay out, in host memory `out` (<= max_jobs of tpg_adam_pack_job_bytes()
- *                           each), one job per owner pack job (`owners`: n_owner pack jobs back to
- *                           back; their w points into `param`) and one per flat element range
- *                           [ranges[2i], ranges[2i] + ranges[2i+1]) updated without an image;
- *                           returns the job count and the launch's block count in *nblocks
- *   tpg_adam_pack_run       run the jobs (copied to device memory): every element of the owned
- *                           parameters and ranges updated exactly as tpg_adam would (same state
- *                           and step conventions), and each owner image written from the updated
- *                           values; a skipped step (grad_check) leaves everything untouched.
- * Images of the parameters that are not their owner are re-packed by tpg_pack_run after it. */
-size_t tpg_adam_pack_job_bytes(void);
-int32_t tpg_adam_pack_owner_ok(const void* job, int64_t numel);
-int32_t tpg_adam_pack_jobs(const void* owners, int32_t n_owner, const int64_t* ranges, int32_t n_ranges,
-                           void* out, int32_t max_jobs, int64_t* nblocks);
-int32_t tpg_adam_pack_run(const void* jobs_dev, int32_t n, int64_t nblocks, float* param, const float* grad,
-                          float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
-                          float weight_decay, int32_t step, float grad_scale, float* state, tpg_stream_t stream);
 
 /* Overflow guard of the loss-scaled fp16 step (torch.cuda.amp.GradScaler's skip): state[3] :=
  * 1 if any of grad[0..numel) is inf / NaN, else 0 (device-side, graph-capturable).  A tpg_adam

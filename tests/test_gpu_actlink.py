@@ -152,65 +152,3 @@ def test_link_discriminator_bf16(gpu):
             tpgan_ops.ACT_LINK["enabled"] = True
     for a, b in zip(res[True], res[False]):
         assert rel(a, b) < 2e-2, rel(a, b)
-
-
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-@pytest.mark.parametrize("cons", [(3, 1, 16), (5, 1, 32)], ids=["3x3", "5x5"])
-def test_link_through_concat(gpu, dtype, cons):
-    """cat([leaky conv, relu transposed conv, an input without a producer]) -> conv (the decoder's
-    enhance_features_* inputs, D_and_G_model.py:309-325): the consumer's epilogue applies the
-    per-channel slopes (TPG_ACT_CHANNEL), each producer takes its channel slice.  On == off."""
-    import tpgan_ops
-    k, s, hw = cons
-    gen = torch.Generator().manual_seed(11 + k)
-    cl = torch.channels_last
-
-    def rnd(*shape, scale=1.0):
-        return ((torch.rand(*shape, generator=gen) * 2 - 1) * scale).to(gpu)
-
-    x0, z0, e0 = rnd(2, 24, hw, hw), rnd(2, 40, hw // 2, hw // 2), rnd(2, 5, hw, hw)
-    wa, ba = rnd(48, 24, 3, 3, scale=0.2), rnd(48, scale=0.1)
-    wt, bt = rnd(40, 32, 3, 3, scale=0.2), rnd(32, scale=0.1)
-    wc, bc = rnd(64, 85, k, k, scale=0.1), rnd(64, scale=0.1)
-    res = {}
-    cat_prev = tpgan_ops.CAT_LINK["enabled"]
-    tpgan_ops.CAT_LINK["enabled"] = True  # (off by default: measured slower on the train step)
-    try:
-        _concat_runs(gpu, dtype, k, cl, (x0, z0, e0, wa, ba, wt, bt, wc, bc), res)
-    finally:
-        tpgan_ops.CAT_LINK["enabled"] = cat_prev
-    for i, (a, b) in enumerate(zip(res[True], res[False])):
-        if dtype == torch.float32 and i not in (4, 6):
-            assert torch.equal(a, b), (i, rel(a, b))
-        elif dtype == torch.float32:
-            # (biases: with its gradient arriving masked, the transposed conv sums its bias in a
-            # column-sum launch instead of the activation-backward pass -- another fp32 order)
-            assert rel(a, b) < 1e-5, (i, rel(a, b))
-        else:
-            assert rel(a, b) < 1e-2, (i, rel(a, b))
-
-
-def _concat_runs(gpu, dtype, k, cl, base, res):
-    import tpgan_ops
-    x0, z0, e0, wa, ba, wt, bt, wc, bc = base
-    for on in (True, False, True):
-        tpgan_ops.ACT_LINK["enabled"] = on
-        try:
-            leaves = [t.contiguous(memory_format=cl).clone().requires_grad_(True) if t.dim() == 4 else
-                      t.clone().requires_grad_(True) for t in (x0, z0, e0, wa, ba, wt, bt, wc, bc)]
-            x, z, e, a_w, a_b, t_w, t_b, c_w, c_b = leaves
-            with tpgan_ops.compute_dtype(dtype), tpgan_ops.deterministic(dtype == torch.float32):
-                ha = tpgan_ops.conv2d(x, a_w, a_b, pad=(1, 1, 1, 1), act=torch.nn.LeakyReLU(0.01))
-                ht = tpgan_ops.conv2d(z, t_w, t_b, stride=(2, 2), pad=(1, 1, 1, 1), act=torch.nn.ReLU(),
-                                      transposed=True, output_padding=(1, 1))
-                h = tpgan_ops.cat([ha, ht, tpgan_ops.to_cl(e, tpgan_ops.get_compute_dtype())],
-                                  act_in_ok=(True, True, False))
-                assert (getattr(h, "_tpg_act_tok", None) is not None) == on
-                y = tpgan_ops.conv2d(h, c_w, c_b, pad=(k // 2,) * 4, act=torch.nn.LeakyReLU(0.01), act_in_ok=True)
-                gy = torch.cos(torch.arange(y.numel(), device=gpu, dtype=torch.float32) * 0.23).reshape(y.shape)
-                y.backward(gy.to(y.dtype))
-            torch.cuda.synchronize()
-            # (e reaches the concat through a dtype conversion in bf16, which has no gradient)
-            res[on] = [t.grad.float().cpu() if t.grad is not None else torch.zeros(1) for t in leaves]
-        finally:
-            tpgan_ops.ACT_LINK["enabled"] = True

@@ -392,12 +392,10 @@ def test_prepacked_weights_match_inline_packing(gpu):
     tr.step(b)  # (the first step also re-lays the flat buffers out in gradient-completion order)
     tr.step(b)
     torch.cuda.synchronize()
-    # images re-packed after the update: by the fused update + one batched table for the rest
-    # (tpgan_ops.adam_pack), one batched table for the whole network, or per bucket when G's
-    # Adam ran bucket by bucket under the backward (TPGANTrainer.overlap_optimizer)
+    # images re-packed after the update: one batched table for the whole network, or per bucket
+    # when G's Adam ran bucket by bucket under the backward (TPGANTrainer.overlap_optimizer)
     assert len(tr.fG.pack_entries) > 50
-    assert (getattr(tr.fG, "adam_pack_table", None) is not None or tr.fG.pack_table is not None or
-            (tr.overlap_optimizer and tr.fG.range_packs[1]))
+    assert tr.fG.pack_table is not None or (tr.overlap_optimizer and tr.fG.range_packs[1])
 
     def run():
         x = b["I128"].clone().requires_grad_(True)
@@ -663,39 +661,3 @@ def test_config5_fp16_256_step(gpu):
     a, c = res[torch.float32], res[torch.float16]
     assert abs(c[0] - a[0]) <= 2e-2 * abs(a[0])
     assert rel(c[1], a[1]) < 1e-1 and rel(c[2], a[2]) < 1e-1, (rel(c[1], a[1]), rel(c[2], a[2]))
-
-
-def test_fused_adam_pack_bit_identical(gpu):
-    """tpg_adam_pack_run (the update writing each parameter's owner weight image, the other
-    images re-packed after it) against tpg_adam + the batched repack: parameters, both moments
-    and every pre-packed image bit for bit, after a bf16 step from the same state; and most of
-    G's parameters are owned (their image is written by the update)."""
-    import tpgan_ops
-    import tpgan_train
-    G, D = _models(gpu)
-    tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False)
-    b = tpgan_train.synthetic_batch(4, gpu, seed=5)
-    tr.step(b)
-    torch.cuda.synchronize()
-    snap = _snapshot(tr)
-    res = {}
-    prev = tpgan_ops.FUSED_ADAM_PACK["enabled"]
-    for fused in (False, True):
-        _restore(tr, snap)
-        tpgan_ops.FUSED_ADAM_PACK["enabled"] = fused
-        try:
-            with tpgan_ops.deterministic():
-                tr.step(b)
-            torch.cuda.synchronize()
-        finally:
-            tpgan_ops.FUSED_ADAM_PACK["enabled"] = prev
-        res[fused] = ([t.clone() for f in (tr.fG, tr.fD) for t in (f.data, f.exp_avg, f.exp_avg_sq)],
-                      {(i, k): e.buf.clone() for i, f in enumerate((tr.fG, tr.fD)) for k, e in f.pack_entries.items()
-                       if e is not None})
-    for a, c in zip(res[False][0], res[True][0]):
-        assert torch.equal(a, c)
-    assert res[False][1].keys() == res[True][1].keys()
-    for k in res[False][1]:
-        assert torch.equal(res[False][1][k], res[True][1][k]), k
-    n_owner = tpgan_ops._adam_pack_table(tr.fG)[7]
-    assert n_owner > 100, n_owner  # (G: 158 conv weights, most of them owned)

@@ -70,33 +70,6 @@ def main():
             ma, mp = statistics.median(ta), statistics.median(tp)
             print("%s var %2d  adam %.3f ms (%.2f TB/s, %d params x 28 B)  pack %.3f ms (%d images, %.0f MB written)  %s"
                   % (name, var, ma, n * 28 / ma / 1e9, n, mp, len(images), pbytes / 1e6, same), flush=True)
-        # the fused update (tpgan_ops.adam_pack): its kernel, then the images no update owns
-        import ctypes
-        from tpgan_lib import check, load, stream_ptr
-        lib = load()
-        dev_j, nj, nb, rdev, rn, rnb, _, n_owner = tpgan_ops._adam_pack_table(f)
-        tf, tr_ = [], []
-        for r in range(a.reps + 2):
-            for t, s in zip((f.data, f.exp_avg, f.exp_avg_sq, f.adam_state), saved):
-                t.copy_(s)
-            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record()
-            check(lib.tpg_adam_pack_run(dev_j.data_ptr(), nj, nb, f.data.data_ptr(), f.grad.data_ptr(),
-                                        f.exp_avg.data_ptr(), f.exp_avg_sq.data_ptr(), 1e-4, 0.5, 0.999, 1e-8, 0.0, 0,
-                                        1.0, f.adam_state.data_ptr(), stream_ptr()))
-            e1.record()
-            if rn:
-                check(lib.tpg_pack_run(rdev.data_ptr(), rn, rnb, stream_ptr()))
-            e2.record()
-            torch.cuda.synchronize()
-            if r >= 2:
-                tf.append(e0.elapsed_time(e1))
-                tr_.append(e1.elapsed_time(e2))
-        same = (all(torch.equal(x, y) for x, y in zip((f.data, f.exp_avg, f.exp_avg_sq), ref[:3])) and
-                all(torch.equal(e.buf, y) for e, y in zip(images, ref[3])))
-        print("%s fused adam+owner pack %.3f ms (%d owners, %d jobs, %d blocks)  rest pack %.3f ms (%d jobs)  %s"
-              % (name, statistics.median(tf), n_owner, nj, nb, statistics.median(tr_), rn,
-                 "bit-exact" if same else "DIFFERS"), flush=True)
         for t, s in zip((f.data, f.exp_avg, f.exp_avg_sq, f.adam_state), saved):
             t.copy_(s)
     os.environ.pop("TPG_OPT_VAR", None)

@@ -1,7 +1,7 @@
 """bench.py with tpgan_ops module switches set first (for same-box kernel-trace A/Bs under
 rocprofv3, which must launch python3 on a script directly):
 
-    python tools/bench_variant.py CAT_LINK=0 tpgan_train.IDENTITY_STREAM=0 -- --steps 10 --no-cpu-baseline
+    python tools/bench_variant.py ACT_LINK=0 tpgan_train.IDENTITY_STREAM=0 -- --steps 10 --no-cpu-baseline
 """
 import os
 import sys

@@ -58,10 +58,9 @@ class LocalPathway(nn.Module):
         conv2 = self.conv2(conv1)
         conv3 = self.conv3(conv2)
         deconv0 = self.deconv0(conv3)
-        # (act_in_ok: deconv0 / deconv1 feed these concats alone, tpgan_ops.CatToken)
-        after_select0 = self.after_select0(tpgan_ops.cat([deconv0, conv2], act_in_ok=(True, False)), act_in_ok=True)
+        after_select0 = self.after_select0(tpgan_ops.cat([deconv0, conv2]), act_in_ok=True)
         deconv1 = self.deconv1(after_select0)
-        after_select1 = self.after_select1(tpgan_ops.cat([deconv1, conv1], act_in_ok=(True, False)), act_in_ok=True)
+        after_select1 = self.after_select1(tpgan_ops.cat([deconv1, conv1]), act_in_ok=True)
         deconv2 = self.deconv2(after_select1)
         after_select2 = self.after_select2(tpgan_ops.cat([deconv2, conv0]))
         local_img = self.local_img(after_select2)
@@ -80,10 +79,10 @@ class LocalPathway(nn.Module):
         conv2 = G([p.conv2 for p in paths], conv1)
         conv3 = G([p.conv3 for p in paths], conv2)
         deconv0 = G([p.deconv0 for p in paths], conv3)
-        after_select0 = G([p.after_select0 for p in paths], [cat([a, b], act_in_ok=(True, False)) for a, b in zip(deconv0, conv2)],
+        after_select0 = G([p.after_select0 for p in paths], [cat([a, b]) for a, b in zip(deconv0, conv2)],
                           act_in_ok=True)
         deconv1 = G([p.deconv1 for p in paths], after_select0)
-        after_select1 = G([p.after_select1 for p in paths], [cat([a, b], act_in_ok=(True, False)) for a, b in zip(deconv1, conv1)],
+        after_select1 = G([p.after_select1 for p in paths], [cat([a, b]) for a, b in zip(deconv1, conv1)],
                           act_in_ok=True)
         deconv2 = G([p.deconv2 for p in paths], after_select1)
         after_select2 = G([p.after_select2 for p in paths], [cat([a, b]) for a, b in zip(deconv2, conv0)])
@@ -234,19 +233,19 @@ class GlobalPathway(nn.Module):
         assert enhance_features_8.shape[2] == self.img_size // 16  # :301
         upsample_16 = self.upsample_16(enhance_features_8, act_in_ok=True)
         add_conv_and_deconv_16 = self.add_conv_and_deconv_16(conv3)
-        enhance_features_16 = self.enhance_features_16(cat([upsample_16, add_conv_and_deconv_16], act_in_ok=(True, True)),
+        enhance_features_16 = self.enhance_features_16(cat([upsample_16, add_conv_and_deconv_16]),
                                                        act_in_ok=True)
         assert enhance_features_16.shape[2] == self.img_size // 8  # :308
         upsample_32 = self.upsample_32(enhance_features_16, act_in_ok=True)
         add_conv_and_deconv_32 = self.add_conv_and_deconv_32(cat([deconv_32, conv2]))
-        enhance_features_32 = self.enhance_features_32(cat([upsample_32, add_conv_and_deconv_32], act_in_ok=(True, True)),
+        enhance_features_32 = self.enhance_features_32(cat([upsample_32, add_conv_and_deconv_32]),
                                                        act_in_ok=True)
         upsample_64 = self.upsample_64(enhance_features_32, act_in_ok=True)
         add_conv_and_deconv_64 = self.add_conv_and_deconv_64(cat([deconv_64, conv1]))
-        enhance_features_64 = self.enhance_features_64(cat([upsample_64, add_conv_and_deconv_64], act_in_ok=(True, True)),
+        enhance_features_64 = self.enhance_features_64(cat([upsample_64, add_conv_and_deconv_64]),
                                                        act_in_ok=True)
         upsample_128 = self.upsample_128(enhance_features_64, act_in_ok=True)
-        add_conv_and_deconv_128 = self.add_conv_and_deconv_128(cat([deconv_128, conv0, I128], act_in_ok=(True, False, False)),
+        add_conv_and_deconv_128 = self.add_conv_and_deconv_128(cat([deconv_128, conv0, I128]),
                                                                act_in_ok=True)
         return upsample_128, add_conv_and_deconv_128, fc2
 
@@ -257,8 +256,7 @@ class GlobalPathway(nn.Module):
         cat = tpgan_ops.cat
         upsample_128, add_conv_and_deconv_128, fc2 = enc
         enhance_features_128 = self.enhance_features_128(
-            cat([upsample_128, add_conv_and_deconv_128, local_feature, local_fake_image],
-                act_in_ok=(True, True, False, False)), act_in_ok=True)
+            cat([upsample_128, add_conv_and_deconv_128, local_feature, local_fake_image]), act_in_ok=True)
         conv5 = self.conv5(enhance_features_128, act_in_ok=True)
         conv6 = self.conv6(conv5, act_in_ok=True)
         decoded_img128 = self.decoded_img128(conv6, act_in_ok=True)

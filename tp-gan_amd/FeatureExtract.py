@@ -56,11 +56,9 @@ class FeatureExtractModel(nn.Module):
         return self.base_model.extract_features(x)
 
 
-# BATCH_REAL: the real images ride in the fake images' extractor pass as one 2B batch (the
-# frozen extractor is in eval mode: a sample's features do not depend on its batch), instead of
-# a separate no-grad pass on a side stream -- the small-map layers are launch-bound, so a 2B
-# launch costs about what a B launch does, and a third of the extractor's launches go away
-BATCH_REAL = {"enabled": False}
+# (BATCH_REAL -- the real images riding in the fake images' extractor pass as one 2B batch --
+# was built in round 4 and removed in round 6: measured slower than the real features on a side
+# stream under G's forward, real_features_async)
 
 
 class IdentityPreservingLoss(nn.Module):
@@ -81,7 +79,7 @@ class IdentityPreservingLoss(nn.Module):
         """Start the real images' features (they do not depend on G) on a side HIP stream,
         planned for a share of the chip, so that they run under G's forward; the handle goes
         to forward(pre=...).  None when there is no GPU side stream to use."""
-        if BATCH_REAL["enabled"] or not (tpgan_ops.MULTISTREAM and real.is_cuda):
+        if not (tpgan_ops.MULTISTREAM and real.is_cuda):
             return None
         main = torch.cuda.current_stream()
         # (a stream of its own: the weight-gradient side stream would queue behind this work)
@@ -94,13 +92,6 @@ class IdentityPreservingLoss(nn.Module):
 
     def forward(self, fake, real, pre=None):
         with tpgan_ops.compute_dtype(self.compute_dtype):
-            if pre is None and BATCH_REAL["enabled"] and fake.shape == real.shape:
-                B = fake.shape[0]
-                both = self.extractor.extract_features(torch.cat([fake, real.detach().to(fake.dtype)], 0))
-                loss = 0.0
-                for f in both:
-                    loss = loss + (f[:B].float() - f[B:].detach().float()).abs().mean()
-                return loss
             if pre is not None:
                 st, fr = pre
                 main = torch.cuda.current_stream()

@@ -55,6 +55,12 @@ static thread_local int g_share = 1;
 #endif
 // forced k-step split of the forward / input-gradient launches (desc.data_ksplit; 0 = planner)
 static thread_local int g_data_ks = 0;
+// paired last k-step in the halo kernel (HaloArgs.half); TPG_HALO_PAIR=0 (read once at load, so
+// every packed image and plan of the process agree) turns it off for same-box A/B runs
+static const int g_halo_pair = [] {
+  const char* e = getenv("TPG_HALO_PAIR");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
 // kernel of the small-map multi-tap forward / input-gradient plans (desc.data_algo; 0 = rule)
 static thread_local int g_data_algo = 0;
 struct ShareScope {
@@ -555,6 +561,9 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   h.A_H = a.A_H; h.A_W = a.A_W; h.C = a.C;
   h.nks = cdiv(a.C, ks_elems);
   h.ntaps = a.ntaps;
+  // (16-bit: a last k-step with <= 16 live channels runs two taps per MFMA; never on the
+  // pointwise kernel, which needs C % 32 == 0)
+  h.half = (half16(dtype) && g_halo_pair && a.C % 32 != 0 && a.C % 32 <= 16) ? 1 : 0;
   h.dymin = dymin; h.dxmin = dxmin;
   h.TH = bth; h.TW = btw; h.IMG = bimg; h.SH = S; h.SW = S; h.dil = a.dil;
   h.HH = (bth - 1) * S + sy; h.HW = (btw - 1) * S + sx;
@@ -609,7 +618,9 @@ static void maybe_halo(Prob& P, int dtype, int N) {
   P.hcfg = cfg;
   P.g_wp = P.wp_bytes;
   P.g_sk = P.sk_bytes;
-  P.wp_bytes = (size_t)rup((int64_t)halo_wp_bytes(h.nks, h.ntaps, bn, h.ntiles), 256);
+  P.wp_bytes = (size_t)rup((int64_t)halo_wp_bytes(h.nks, h.ntaps, bn, h.ntiles, h.half), 256);
+  P.pk.hnks = h.nks;
+  P.pk.half = h.half;
   P.sk_bytes = h.ksplit > 1 ? (size_t)rup((int64_t)h.ksplit * a.M * a.Nout * 4, 256) : 0;
 }
 
@@ -794,7 +805,6 @@ struct HaloXA {
   tpg_tensor X;
   int act;
   float slope;
-  XaSegs segs;          // TPG_ACT_CHANNEL (nseg > 0)
   bool applied;
 };
 
@@ -835,9 +845,6 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
     bool ok = xa->X.data && xa->X.dtype == Y.dtype && xa->X.stride[0] == Y.stride[0] && xa->X.stride[2] == Y.stride[2] &&
               xa->X.stride[3] == Y.stride[3] && xa->X.stride[1] == 1 && vec_ok(xa->X, dtype) == vec_ok(Y, dtype);
     for (const Prob& P : v) ok = ok && P.halo;
-    // (per-channel segment slopes, TPG_ACT_CHANNEL: not in the halo kernel's epilogue -- their
-    // per-element selects spilled its wide tiles -- so always the caller's in-place pass)
-    ok = ok && xa->segs.nseg == 0;
     if (ok) {
       XA = xa->X.data;
       xa->applied = true;
@@ -880,8 +887,6 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
         h.G = mk->G.data; h.mact = mk->act; h.mslope = mk->slope;
       }
       h.XA = XA; h.xa_act = XA ? xa->act : 0; h.xa_slope = XA ? xa->slope : 0.f;
-      if (XA) h.xa_segs = xa->segs;
-      else memset(&h.xa_segs, 0, sizeof(h.xa_segs));
       int e = do_halo(h, dtype, P.hcfg, s, mk != nullptr);
       if (e) return hip_check(e, "halo conv");
       if (h.ksplit > 1) {
@@ -895,7 +900,6 @@ static int32_t run_probs(std::vector<Prob>& v, int dtype, const tpg_tensor& A, c
         ep.R = R.data; ep.r_sn = R.stride[0]; ep.r_sh = R.stride[2]; ep.r_sw = R.stride[3];
         ep.res_scale = res_scale; ep.act = act; ep.slope = slope; ep.dtype = dtype;
         ep.XA = XA; ep.xa_act = XA ? xa->act : 0; ep.xa_slope = XA ? xa->slope : 0.f;
-        if (XA) ep.xa_segs = xa->segs;
         e = do_epilogue(ep, s);
         if (e) return hip_check(e, "halo epilogue");
       }
@@ -988,7 +992,7 @@ extern "C" int32_t tpg_conv2d_pack_jobs(const tpg_conv_desc* d, int32_t op, tpg_
       if (P.halo) {
         j.kind = 1;
         j.nks = P.h.nks; j.bn = P.h.BN; j.bnl = (P.h.BN + 127) / 128 * 128; j.ntiles = P.h.ntiles;
-        j.items = j.nks * j.k.ntaps * j.ntiles * j.bnl * 4;
+        j.items = halo_steps(j.nks, j.k.ntaps, P.h.half) * j.ntiles * j.bnl * 4;
       } else {
         j.kind = 0;
         j.items = j.k.Npad * j.k.nunits;
@@ -1342,18 +1346,7 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
   memset(&xa, 0, sizeof(xa));
   const bool xact = dx.data && d->in_act != TPG_ACT_NONE;
   if (xact) {
-    if (d->in_act < TPG_ACT_NONE || d->in_act > TPG_ACT_CHANNEL) return fail(-2, "conv2d_bwd: bad in_act %d", d->in_act);
-    if (d->in_act == TPG_ACT_CHANNEL) {
-      if (d->in_nseg < 1 || d->in_nseg > 4) return fail(-2, "conv2d_bwd: in_act CHANNEL needs 1..4 segments");
-      for (int k = 0; k < d->in_nseg; ++k)
-        if (d->in_seg_end[k] < (k ? d->in_seg_end[k - 1] : 1)) return fail(-2, "conv2d_bwd: segment ends must increase");
-      xa.segs.nseg = d->in_nseg;
-      for (int k = 0; k < 4; ++k) {  // (unused trailing segments repeat the last one)
-        const int q = k < d->in_nseg ? k : d->in_nseg - 1;
-        xa.segs.end[k] = d->in_seg_end[q];
-        xa.segs.slope[k] = d->in_seg_slope[q];
-      }
-    }
+    if (d->in_act < TPG_ACT_NONE || d->in_act > TPG_ACT_RELU6) return fail(-2, "conv2d_bwd: bad in_act %d", d->in_act);
     if ((rc = check_tensor(x, d->dtype, "x")) || (rc = check_tensor(dx, d->dtype, "dx"))) return rc;
     xa.X = x; xa.act = d->in_act; xa.slope = d->in_slope;
   }
@@ -1404,13 +1397,8 @@ extern "C" int32_t tpg_conv2d_bwd(const tpg_conv_desc* d, tpg_tensor x, tpg_tens
     if ((rc = bwd_data_impl(d, G, w, dx, ws, ws_bytes, stream, xact ? &xa : nullptr))) return rc;
   }
   if (xact && !xa.applied) {  // (plans whose epilogue cannot take it: one in-place pass over dx)
-    if (xa.segs.nseg > 0) {
-      TPG_GROUP_SYNC();
-      rc = hip_check(launch_act_chan_inplace(d->n, d->in_c, d->in_h, d->in_w, x, dx, xa.segs, s), "act_chan (in_act)");
-    } else {
-      rc = hip_check(do_act_bwd(d->n, d->in_c, d->in_h, d->in_w, d->in_act, d->in_slope, dx, x, dx, nullptr, s),
-                     "act_bwd (in_act)");
-    }
+    rc = hip_check(do_act_bwd(d->n, d->in_c, d->in_h, d->in_w, d->in_act, d->in_slope, dx, x, dx, nullptr, s),
+                   "act_bwd (in_act)");
     if (rc) return rc;
   }
   // 3. the weight gradient, summing the bias gradient in the same launch where it can
@@ -1560,81 +1548,6 @@ extern "C" int32_t tpg_adam(int64_t numel, float* param, const float* grad, floa
                                grad_scale, state, (hipStream_t)stream);
   if (rc == -1) return fail(-15, "adam: buffers must be 4-byte aligned, at one offset inside 16 bytes");
   return hip_check(rc, "adam");
-}
-
-// ---- Adam fused with the owner images' packing
-extern "C" size_t tpg_adam_pack_job_bytes(void) { return sizeof(AdamPackJob); }
-
-extern "C" int32_t tpg_adam_pack_owner_ok(const void* job, int64_t numel) {
-  if (!job || numel <= 0) return 0;
-  const PackJob& j = *reinterpret_cast<const PackJob*>(job);
-  const PackArgs& k = j.k;
-  if (j.kind != 1 || (k.dtype != TPG_BF16 && k.dtype != TPG_F16)) return 0;
-  if ((k.cmode == 0 ? k.w_sa : k.w_sb) != 1 || k.cmode == k.nmode || k.cmode > 1 || k.nmode > 1) return 0;
-  if ((int64_t)k.Nreal * k.Creal * k.ntaps != numel || k.ntaps < 1 || k.ntaps > TPG_MAX_TAPS) return 0;
-  if (j.nks * 4 * (16 / (k.dtype == TPG_F32 ? 4 : 2)) < k.Creal || j.bn < 1 || j.ntiles * j.bn < k.Nreal) return 0;
-  // every element exactly once: distinct taps, and the (row, tap) offsets of a dense weight
-  for (int a = 0; a < k.ntaps; ++a)
-    for (int b = a + 1; b < k.ntaps; ++b)
-      if (k.tr[a] == k.tr[b] && k.ts[a] == k.ts[b]) return 0;
-  return 1;
-}
-
-extern "C" int32_t tpg_adam_pack_jobs(const void* owners, int32_t n_owner, const int64_t* ranges, int32_t n_ranges,
-                                      void* out, int32_t max_jobs, int64_t* nblocks) {
-  if (n_owner < 0 || n_ranges < 0 || (n_owner && !owners) || (n_ranges && !ranges) || !out || !nblocks)
-    return fail(-2, "adam_pack_jobs: bad arguments");
-  if (n_owner + n_ranges > max_jobs) return fail(-22, "adam_pack_jobs: more than %d jobs", max_jobs);
-  AdamPackJob* o = reinterpret_cast<AdamPackJob*>(out);
-  int64_t b = 0;
-  int n = 0;
-  for (int i = 0; i < n_owner; ++i) {
-    AdamPackJob& j = o[n++];
-    memset(&j, 0, sizeof(j));
-    memcpy(&j.pj, reinterpret_cast<const char*>(owners) + (size_t)i * sizeof(PackJob), sizeof(PackJob));
-    if (j.pj.kind != 1 || j.pj.items <= 0) return fail(-2, "adam_pack_jobs: owner %d is not a halo-layout image", i);
-    j.kind = 1;
-    // (the kernel's unit: half an 8-channel chunk, 4 elements)
-    j.len = (int64_t)j.pj.k.Nreal * j.pj.k.ntaps * cdiv(j.pj.k.Creal, 8) * 2;
-    if (j.len >= (1ll << 31)) return fail(-2, "adam_pack_jobs: owner %d too large", i);
-    j.nblocks = (int)((j.len + 256 * TPG_PACK_GROUPS - 1) / (256 * TPG_PACK_GROUPS));
-    j.first_block = (int)b;
-    b += j.nblocks;
-  }
-  for (int i = 0; i < n_ranges; ++i) {
-    const int64_t off = ranges[2 * i], len = ranges[2 * i + 1];
-    if (off < 0 || len <= 0) return fail(-2, "adam_pack_jobs: bad range %lld+%lld", (long long)off, (long long)len);
-    AdamPackJob& j = o[n++];
-    memset(&j, 0, sizeof(j));
-    j.kind = 0;
-    j.off = off;
-    j.len = len;
-    // (blocks cover aligned float4 groups from floor(off / 4) on)
-    const int64_t groups = (off + len + 3) / 4 - off / 4;
-    j.nblocks = (int)((groups + TPG_ADAM_RANGE_BLOCK / 4 - 1) / (TPG_ADAM_RANGE_BLOCK / 4));
-    j.first_block = (int)b;
-    b += j.nblocks;
-  }
-  if (b >= (1ll << 31)) return fail(-2, "adam_pack_jobs: too many blocks");
-  *nblocks = b;
-  return n;
-}
-
-extern "C" int32_t tpg_adam_pack_run(const void* jobs_dev, int32_t n, int64_t nblocks, float* param, const float* grad,
-                                     float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
-                                     float weight_decay, int32_t step, float grad_scale, float* state,
-                                     tpg_stream_t stream) {
-  TPG_GROUP_SYNC();
-  if (!state || !param || !grad || !exp_avg || !exp_avg_sq) return fail(-10, "adam_pack: NULL pointer");
-  if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16)
-    return fail(-15, "adam_pack: flat buffers must be 16-byte aligned");
-  if (n < 0 || nblocks < 0 || nblocks >= (1ll << 31) || (n > 0 && !jobs_dev)) return fail(-2, "adam_pack: bad jobs");
-  hipStream_t s = (hipStream_t)stream;
-  int rc = 0;
-  if (step >= 0) rc = launch_adam_sched(state, beta1, beta2, step, s);
-  if (!rc) rc = launch_adam_pack(reinterpret_cast<const AdamPackJob*>(jobs_dev), n, (int)nblocks, param, grad, exp_avg,
-                                 exp_avg_sq, lr, beta1, beta2, eps, weight_decay, state, grad_scale, s);
-  return hip_check(rc, "adam_pack");
 }
 
 extern "C" int32_t tpg_grad_check_impl(int64_t, const float*, float*, hipStream_t);

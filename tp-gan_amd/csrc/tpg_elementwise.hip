@@ -125,33 +125,6 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restric
   }
 }
 
-// one thread per (pixel, channel): the rare fallback of the per-channel input-gradient act'
-__global__ __launch_bounds__(256) void act_chan_kernel(int64_t total, int c, int w, int h, tpg_tensor x, tpg_tensor dx,
-                                                        const XaSegs sg) {
-  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
-  if (i >= total) return;
-  const int ch = (int)(i % c);
-  int64_t pix = i / c;
-  const int px = (int)(pix % w);
-  pix /= w;
-  const int py = (int)(pix % h);
-  const int64_t n = pix / h;
-  const int64_t xo = n * x.stride[0] + py * x.stride[2] + px * x.stride[3] + ch;
-  const int64_t go = n * dx.stride[0] + py * dx.stride[2] + px * dx.stride[3] + ch;
-  const float xv = ld_any(x.data, x.dtype, xo);
-  const float gv = ld_any(dx.data, dx.dtype, go);
-  st_any(dx.data, dx.dtype, go, tpg_xa_grad(gv, xv, 0, 0.f, sg, ch));
-}
-
-int launch_act_chan_inplace(int n, int c, int h, int w, const tpg_tensor& x, const tpg_tensor& dx, const XaSegs& sg,
-                            hipStream_t s) {
-  const int64_t total = (int64_t)n * h * w * c;
-  if (total <= 0) return 0;
-  hipLaunchKernelGGL(act_chan_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, c, w, h, x, dx,
-                     sg);
-  return (int)hipGetLastError();
-}
-
 int launch_pack_many(const PackJob* jobs_dev, int n, int nblocks, hipStream_t s) {
   if (n <= 0 || nblocks <= 0) return 0;
   hipLaunchKernelGGL(pack_many_kernel, dim3(nblocks), dim3(256), 0, s, jobs_dev, n);
@@ -702,147 +675,6 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
     adam_one(p[i], gr[i], gscale, m[i], v[i], lr_bc1, b1, b2, eps, wd, bc2s);
 }
 
-// ---- Adam fused with the owner images' packing (tpg_adam_pack_run).  Block b finds its job
-// (binary search over first_block, as pack_many_kernel).  Range job: TPG_ADAM_RANGE_BLOCK
-// elements per block in aligned float4 groups (a group straddling the range's ends updates only
-// its elements inside).  Owner job: TPG_PACK_GROUPS * 256 half chunks per block; a chunk is EPC
-// consecutive channels of one weight row and tap, i.e. EPC consecutive parameter elements,
-// enumerated in the parameter's own order (a first version walked the IMAGE order: rows of one
-// tap 20 KB apart in the master, 2.0 ms for G against 0.66 + 0.51 ms for Adam + pack): they are
-// updated (the same adam_one as adam_kernel) and their image chunk written from the new values
-// (the conversion pack_halo_item applies) -- no second read of the fp32 master for that image.
-template <typename E>
-__device__ __forceinline__ void adam_pack_half(const PackArgs& k, int bn, int bnl, int ntiles, int i, float* P,
-                                               const float* G, float* M, float* V, float lr_bc1, float b1, float b2,
-                                               float eps, float wd, float bc2s, float gscale) {
-  // i enumerates HALF chunks (4 elements, one float4) in the parameter's own order -- row np
-  // slowest, then tap, then channel -- so the 64 lanes of a wave read 1 KB of each buffer
-  // contiguously (a version with one 8-element chunk per lane spread every float4 load over
-  // twice the cache lines and ran at half the plain update's rate); each lane writes its 8-byte
-  // half of the image chunk.  (32-bit index math: a parameter has < 2^31 half chunks; the
-  // images' padding rows were zeroed when first packed and are never written here.)
-  constexpr int EPC = 16 / sizeof(E);
-  static_assert(EPC == 8, "16-bit images");
-  constexpr int ROW = 4 * EPC;
-  const int CC2 = 2 * ((k.Creal + EPC - 1) / EPC);
-  const int rt = i / CC2;
-  const int hh = i - rt * CC2;
-  const int np = rt / k.ntaps;
-  const int tap = rt - np * k.ntaps;
-  const int cc = hh >> 1, half = hh & 1;
-  const int c0 = cc * EPC + half * 4;
-  const int nt = np / bn, r = np - nt * bn;
-  const int ks = (cc * EPC) / ROW, lc = cc - ks * 4;
-  const int64_t idx = ((((int64_t)ks * k.ntaps + tap) * ntiles + nt) * bnl + r) * 4 + (lc ^ pack_hswz(r));
-  const int64_t base = (int64_t)k.tr[tap] * k.w_sr + (int64_t)k.ts[tap] * k.w_ss +
-                       (k.nmode == 0 ? (int64_t)np * k.w_sa : (int64_t)np * k.w_sb);
-  const int64_t e0 = (k.W - P) + base + c0;  // element index in the flat buffers (unit channel stride)
-  const int nv = min(4, k.Creal - c0);       // (<= 0: the padding half of the row's last chunk)
-  union { uint2 u; E e[4]; } o;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) o.e[e] = (E)0.f;
-  if (nv == 4 && (e0 & 3) == 0) {
-    tpg_f4 pv = adam_ld<true>(P + e0, 0), g = adam_ld<true>(G + e0, 0), mv = adam_ld<true>(M + e0, 0),
-           vv = adam_ld<true>(V + e0, 0);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pv[e], me = mv[e], ve = vv[e];
-      adam_one(pe, g[e], gscale, me, ve, lr_bc1, b1, b2, eps, wd, bc2s);
-      pv[e] = pe; mv[e] = me; vv[e] = ve;
-      o.e[e] = (E)pe;
-    }
-    adam_st<true>(P + e0, 0, pv);
-    adam_st<true>(M + e0, 0, mv);
-    adam_st<true>(V + e0, 0, vv);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (e < nv) {
-        float pe = P[e0 + e], me = M[e0 + e], ve = V[e0 + e];
-        adam_one(pe, G[e0 + e], gscale, me, ve, lr_bc1, b1, b2, eps, wd, bc2s);
-        P[e0 + e] = pe; M[e0 + e] = me; V[e0 + e] = ve;
-        o.e[e] = (E)pe;
-      }
-    }
-  }
-  reinterpret_cast<uint2*>(k.Wp)[idx * 2 + half] = o.u;
-}
-
-__global__ __launch_bounds__(256) void adam_pack_kernel(const AdamPackJob* __restrict__ jobs, int n, float* P,
-                                                        const float* G, float* M, float* V, float lr, float b1,
-                                                        float b2, float eps, float wd, const float* __restrict__ st,
-                                                        float gscale) {
-  if (st[3] != 0.f) return;  // non-finite gradients this step (grad_finite_kernel)
-  const float lr_bc1 = lr / st[1], bc2s = st[2];
-  __shared__ AdamPackJob job;
-  __shared__ int jsel;
-  if (threadIdx.x == 0) {
-    int lo = 0, hi = n - 1;
-    const int b = blockIdx.x;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].first_block <= b) lo = mid; else hi = mid - 1;
-    }
-    jsel = lo;
-  }
-  __syncthreads();
-  {
-    const int* src = reinterpret_cast<const int*>(jobs + jsel);
-    int* dst = reinterpret_cast<int*>(&job);
-    for (int i = threadIdx.x; i < (int)(sizeof(AdamPackJob) / 4); i += 256) dst[i] = src[i];
-  }
-  __syncthreads();
-  const int lb = blockIdx.x - job.first_block;
-  if (job.kind == 0) {
-    const int64_t lo = job.off, hi = job.off + job.len;
-    const int64_t g0 = (lo >> 2) + (int64_t)lb * (TPG_ADAM_RANGE_BLOCK / 4);  // float4 groups (absolute)
-#pragma unroll 1
-    for (int it = 0; it < TPG_ADAM_RANGE_BLOCK / 1024; ++it) {
-      const int64_t q = g0 + it * 256 + threadIdx.x;
-      const int64_t e0 = q * 4;
-      if (e0 >= hi) break;
-      if (e0 >= lo && e0 + 4 <= hi) {
-        tpg_f4 pv = adam_ld<true>(P, q), g = adam_ld<true>(G, q), mv = adam_ld<true>(M, q), vv = adam_ld<true>(V, q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float pe = pv[e], me = mv[e], ve = vv[e];
-          adam_one(pe, g[e], gscale, me, ve, lr_bc1, b1, b2, eps, wd, bc2s);
-          pv[e] = pe; mv[e] = me; vv[e] = ve;
-        }
-        adam_st<true>(P, q, pv);
-        adam_st<true>(M, q, mv);
-        adam_st<true>(V, q, vv);
-      } else {
-        for (int64_t i = e0 > lo ? e0 : lo; i < e0 + 4 && i < hi; ++i)
-          adam_one(P[i], G[i], gscale, M[i], V[i], lr_bc1, b1, b2, eps, wd, bc2s);
-      }
-    }
-    return;
-  }
-  const PackJob& pj = job.pj;
-#pragma unroll 1
-  for (int g = 0; g < TPG_PACK_GROUPS; ++g) {
-    const int idx = (lb * TPG_PACK_GROUPS + g) * 256 + threadIdx.x;
-    if (idx >= (int)job.len) break;  // (owner: len = the parameter's half chunks, < 2^31)
-    if (pj.k.dtype == TPG_F16)
-      adam_pack_half<_Float16>(pj.k, pj.bn, pj.bnl, pj.ntiles, idx, P, G, M, V, lr_bc1, b1, b2, eps, wd, bc2s, gscale);
-    else
-      adam_pack_half<__bf16>(pj.k, pj.bn, pj.bnl, pj.ntiles, idx, P, G, M, V, lr_bc1, b1, b2, eps, wd, bc2s, gscale);
-  }
-}
-
-int launch_adam_pack(const AdamPackJob* jobs, int n, int nblocks, float* p, const float* g, float* m, float* v,
-                     float lr, float b1, float b2, float eps, float wd, const float* st, float gscale, hipStream_t s) {
-  if (n <= 0 || nblocks <= 0) return 0;
-  hipLaunchKernelGGL(adam_pack_kernel, dim3(nblocks), dim3(256), 0, s, jobs, n, p, g, m, v, lr, b1, b2, eps, wd, st,
-                     gscale);
-  return (int)hipGetLastError();
-}
-
-int launch_adam_sched(float* st, float b1, float b2, int host_step, hipStream_t s) {
-  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, s, st, b1, b2, host_step);
-  return (int)hipGetLastError();
-}
 
 // st[3] := 1 when any gradient element is inf / NaN (st[3] zeroed by a memset node first; every
 // writer stores the same value, so the race is benign).  HBM-bound: 4 B per element.

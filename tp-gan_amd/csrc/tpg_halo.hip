@@ -55,17 +55,11 @@ __host__ __device__ constexpr int halo_bnl(int bn) { return (bn + 127) / 128 * 1
 __host__ __device__ constexpr int halo_epi_rows(int bn, int bm = 256) {
   return bm == 512 ? 256 : bn >= 192 ? 64 : bn >= 80 ? 128 : 256;
 }
-// Column-half passes for the 208-wide tile (8 x 1 waves, 13 fragments per wave: every wave
-// parks its first 7 fragments, then its last 6) -- built and measured, not used: 1.5 % faster
-// per enhance_128 launch than four 64-row passes, but every 416-byte pixel row is then written
-// (and its residual read) in two passes, so the 128-byte lines at the split are touched twice:
-// HBM traffic 895 -> 990 MB per launch (1.36x -> 1.51x algorithmic, gpurun r05ao PMC)
-#ifndef TPG_HALO_COLP
-#define TPG_HALO_COLP 0
-#endif
-__host__ __device__ constexpr bool halo_epi_colp(int bn) { return TPG_HALO_COLP && bn == 208; }
+// (Column-half passes for the 208-wide tile were built in round 5 and removed in round 6: 1.5 %
+// faster per launch, but every 416-byte pixel row was written and its residual read in two
+// passes: HBM traffic 895 -> 990 MB per enhance_128 launch, gpurun r05ao PMC.)
 __host__ __device__ constexpr int halo_epi_acc_bytes(int bn, int bm = 256) {
-  return halo_epi_colp(bn) ? bm * ((bn / 16 + 1) / 2 * 16 + 4) * 4 : halo_epi_rows(bn, bm) * (bn + 4) * 4;
+  return halo_epi_rows(bn, bm) * (bn + 4) * 4;
 }
 // (row-offset table [BM][2] int64 + bias [256] floats, then the parked accumulators)
 __host__ __device__ constexpr int halo_epi_lds(int bn, int bm = 256) { return bm * 16 + 1024 + halo_epi_acc_bytes(bn, bm); }
@@ -233,9 +227,15 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     for (int j = 0; j < GL; ++j) lds_dma16(src + j * 1024, d0 + j * 1024);
   };
 
+  // pipeline steps: ntaps per k-step; with p.half the problem's last k-step (when this block's
+  // k range ends there) is paired, ceil(ntaps / 2) steps (see compute)
+  const int ntaps = p.ntaps;
+  const bool lastp = BF && p.half && ks0 + nks == p.nks && nks > 0;
+  const int npair_b = lastp ? (ntaps + 1) >> 1 : 0;
+  const int steps_full = (lastp ? nks - 1 : nks) * ntaps;
   // the first two steps' weight DMAs go out before the halo index math (they need none of
   // it), so their latency runs under it
-  const int total = nks * p.ntaps;
+  const int total = steps_full + npair_b;
   if (total > 0) {
     issue_w(0, 0);
     issue_w(min(1, total - 1), 1);
@@ -365,25 +365,6 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll
     for (int n = 0; n < NREP; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Stagger (bf16, BN >= 128 tiles, which run one block per CU anyway): waves 4-7 carry the MFMAs of B fragments NH.. of every step over the barrier
-  // (operands held in registers, +28 VGPRs) and issue them first in the next step, so each
-  // SIMD has matrix work while its partner wave waits for the step's fragment reads
-  // (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Measured ~1 % on the 128x128 layers.
-  // (off since round 3: with the leaner step body the carried MFMAs' register copies cost
-  // more than the overlap gave -- dgrad enhance_128 1.115 -> 1.081 ms, step 35.71 -> 35.63 ms
-  // same box; -DTPG_HALO_LAG builds it back in)
-#ifdef TPG_HALO_LAG
-  constexpr bool LAG_OK = BF && BN >= 128;
-#else
-  constexpr bool LAG_OK = false;
-#endif
-  constexpr int NH = LAG_OK ? (NREP + 1) / 2 : NREP;
-  const bool lag = LAG_OK && wave >= 4;
-  u32x4 ha[MREP], hb[NREP - NH + 1];
-#pragma unroll
-  for (int m = 0; m < MREP; ++m) ha[m] = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int n = 0; n < NREP - NH; ++n) hb[n] = u32x4{0u, 0u, 0u, 0u};
   auto mma = [&](u32x4 a, u32x4 b, f32x4 c) -> f32x4 {
     if constexpr ((TPG_HALO_ABL & 4) != 0) {
       c[0] += __builtin_bit_cast(float, a[0] ^ b[1]);
@@ -398,23 +379,25 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       return c;
     }
   };
-  auto held_mfmas = [&]() {
-    if constexpr (LAG_OK)
-#pragma unroll
-    for (int n = NH; n < NREP; ++n)
-#pragma unroll
-      for (int m = 0; m < MREP; ++m) acc[m][n] = mma(ha[m], hb[n - NH], acc[m][n]);
-  };
 
-  auto compute = [&](int hbuf, int wslot, int toff) {
+  // One pipeline step: the A fragments from the halo at tap offset toff (lanes g = 0..3 read
+  // chunks g of the 64-byte pixel rows), the B fragments from ring slot wslot.
+  // Paired step (p.half: the last k-step holds <= 16 live channels, C % 32 in 1..16): K = 32
+  // of one MFMA is channels 0..15 of TWO taps -- lanes g = 0, 1 read chunks 0, 1 at tap offset
+  // toff, lanes g = 2, 3 read chunks 0, 1 at toff2 (the packed slice holds the two taps'
+  // weights in the same chunk order) -- so that k-step runs ceil(ntaps / 2) steps instead of
+  // ntaps half-empty ones (206 channels: 6.9 % fewer MFMAs, 75 / 80: 17 %).
+  auto compute = [&](int hbuf, int wslot, int toff, int toff2, bool paired) {
     const u32x4* H = halo + hbuf * hcap * 4;
     const u32x4* Wl = wts + wslot * BNL * 4;
+    const int tl = g < 2 ? toff : toff2;
+    const int gc = paired ? (g16 & 16) : g16;
     u32x4 af[MREP];
 #pragma unroll
     for (int m = 0; m < MREP; ++m) {
-      // byte offset hp * 64 + 16 * (g ^ hswz(hp)) = (hp << 6) + ((g << 4) ^ ((hp << 3) & 32))
-      const int hp = hbase[m] + toff;
-      af[m] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(H) + (hp << 6) + (g16 ^ ((hp << 3) & 32)));
+      // byte offset hp * 64 + 16 * (chunk ^ hswz(hp)) = (hp << 6) + ((chunk << 4) ^ ((hp << 3) & 32))
+      const int hp = hbase[m] + tl;
+      af[m] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(H) + (hp << 6) + (gc ^ ((hp << 3) & 32)));
     }
     // all B fragments of the step are read up front into their own registers: reusing one
     // register quad across n made hipcc wait (lgkmcnt(0)) before every B read, exposing
@@ -425,28 +408,14 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       const int r = wn * WTN + n * 16 + l16;
       bf[n] = Wl[r * 4 + (g ^ hswz(r))];
     }
-    if (LAG_OK && lag) {
-      held_mfmas();  // previous step's tail: operands already in registers
 #pragma unroll
-      for (int n = 0; n < NH; ++n)
+    for (int n = 0; n < NREP; ++n)
 #pragma unroll
-        for (int m = 0; m < MREP; ++m) acc[m][n] = mma(af[m], bf[n], acc[m][n]);
-#pragma unroll
-      for (int m = 0; m < MREP; ++m) ha[m] = af[m];
-#pragma unroll
-      for (int n = NH; n < NREP; ++n) hb[n - NH] = bf[n];
-      __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP, 0);
-    } else {
-#pragma unroll
-      for (int n = 0; n < NREP; ++n)
-#pragma unroll
-        for (int m = 0; m < MREP; ++m) acc[m][n] = mma(af[m], bf[n], acc[m][n]);
-      // schedule: every fragment read first, then the MFMAs (counted lgkmcnt waits instead
-      // of one full wait per B fragment)
-      __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP * (BF ? 1 : 4), 0);
-    }
+      for (int m = 0; m < MREP; ++m) acc[m][n] = mma(af[m], bf[n], acc[m][n]);
+    // schedule: every fragment read first, then the MFMAs (counted lgkmcnt waits instead
+    // of one full wait per B fragment)
+    __builtin_amdgcn_sched_group_barrier(0x100, MREP + NREP, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, MREP * NREP * (BF ? 1 : 4), 0);
   };
 
   // Software pipeline over steps s = ks*ntaps + t, one barrier per step:
@@ -492,7 +461,6 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     if (tid >= 512 - BN) s_bias[tid - (512 - BN)] = bias_pre;  // (the highest threads: BM >= 256 > BN)
   };
 
-  const int ntaps = p.ntaps;
   // (the tap table written at entry is read only after the prologue's closing barrier)
   if (total > 0) {
     load_halo(0);
@@ -504,7 +472,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     TPG_TL_MARK(1);
     int ks = 0, t = 0, slot = 0;
     int toff = s_toff[0];
-    for (int s = 0; s < total; ++s) {
+    for (int s = 0; s < steps_full; ++s) {
       const bool more_ks = ks + 1 < nks;
       if (t == 0) {
         store_g();  // g of k-step ks (staged at the end of the previous one)
@@ -515,7 +483,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       }
       const int slot2 = slot == 0 ? 2 : slot - 1;  // (s + 2) % 3
       const int toff_next = s_toff[t + 1 == ntaps ? 0 : t + 1];  // read ahead of its use
-      compute(ks & 1, slot, toff);
+      compute(ks & 1, slot, toff, toff, false);
       // step s+2's weight DMA behind this step's fragment reads and MFMAs (it has until the end of
       // step s+1): issued ahead of them it delayed the reads the first MFMAs wait on -- 1-3.5 %
       // per layer (r04: enhance_128 fwd 1.153 -> 1.142 ms, add_128 0.416 -> 0.401)
@@ -527,6 +495,17 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
       slot = slot == 2 ? 0 : slot + 1;
       if (++t == ntaps) { t = 0; ++ks; }
     }
+    // the paired last k-step (halo staged by the last full step; ks == nks - 1 here)
+    for (int j = 0; j < npair_b; ++j) {
+      const int s = steps_full + j;
+      if (j == 0) store_g();
+      const int slot2 = slot == 0 ? 2 : slot - 1;
+      compute(ks & 1, slot, s_toff[2 * j], s_toff[min(2 * j + 1, ntaps - 1)], true);
+      issue_w(min(s + 2, total - 1), slot2);
+      if constexpr (GL == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)" HALO_BAR ::: "memory");
+      slot = slot == 2 ? 0 : slot + 1;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped tail DMA
   } else if constexpr (EARLY) {
     epi_table();
@@ -534,25 +513,18 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   }
   TPG_TL_MARK(2);
 
-  if (lag) held_mfmas();  // the last step's carried MFMAs
-
   // ---- epilogue through LDS: the fp32 accumulators of RP rows at a time are parked in LDS,
   // then every thread finishes 8-channel groups of whole pixel rows: bias, residual and
   // activation with 16-byte residual loads / output stores (or an fp32 partial slice row).
   // Row addresses are computed once per block into a table.
-  // passes: RP rows of all BN columns (the waves owning them park), or for the 208-wide tile
-  // (halo_epi_colp) two column halves in which every wave parks a part of its fragments
-  constexpr bool COLP = halo_epi_colp(BN);
-  static_assert(!COLP || WN == 1, "column passes: one wave column");
-  constexpr int RP = COLP ? BM : halo_epi_rows(BN, BM);  // rows per pass
-  constexpr int NPASS = COLP ? 2 : BM / RP;
-  constexpr int NHP = COLP ? (NREP + 1) / 2 : NREP;       // fragments parked in pass 0
-  constexpr int PW0 = NHP * 16 * (COLP ? 1 : WN), PW1 = COLP ? (NREP - NHP) * 16 : PW0;  // pass columns
-  constexpr int LDW = PW0 + 4;               // padded fp32 row stride
-  constexpr int CG0 = PW0 / 8, CG1 = PW1 / 8;  // 8-channel groups per row of a pass
+  // passes: RP rows of all BN columns (the waves owning them park)
+  constexpr int RP = halo_epi_rows(BN, BM);  // rows per pass
+  constexpr int NPASS = BM / RP;
+  constexpr int LDW = BN + 4;                // padded fp32 row stride
+  constexpr int CG0 = BN / 8;                // 8-channel groups per row of a pass
   constexpr int IPT = (RP * CG0 + 511) / 512;  // groups per thread per pass (the last partial)
   constexpr int NV = 8 * (int)sizeof(E) / 16;  // 16-byte vectors per group
-  static_assert(RP % WTM == 0 && (COLP || PW0 == BN), "epilogue tiling");
+  static_assert(RP % WTM == 0, "epilogue tiling");
   static_assert(halo_epi_acc_bytes(BN, BM) == RP * LDW * 4, "epilogue LDS");
   float* s_acc = reinterpret_cast<float*>(lds) + (EARLY ? 0 : BM * 4 + 256);  // [RP][LDW]
   E* Y = reinterpret_cast<E*>(p.Y);
@@ -560,10 +532,9 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   const E* XA = reinterpret_cast<const E*>(p.XA);
   // group it of a pass -> (table row, column in the pass) (compile-time divisors)
   auto grp = [&](int pass, int it, int& trow, int& c0) __attribute__((always_inline)) {
-    const int cg = (COLP && pass) ? CG1 : CG0;
-    const int row = (COLP && pass) ? it / CG1 : it / CG0;
-    c0 = (it - row * cg) * 8;
-    trow = COLP ? row : pass * RP + row;
+    const int row = it / CG0;
+    c0 = (it - row * CG0) * 8;
+    trow = pass * RP + row;
     return row;
   };
   // residual (or, without one, producer-x) vectors of a pass's groups: bf16 prefetches them,
@@ -577,8 +548,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
   const bool pvec = pf_r ? p.rvec : p.yvec;
   u32x4 pv[IPT][NV];
   auto prefetch = [&](int pass) __attribute__((always_inline)) {
-    const int ng = RP * ((COLP && pass) ? CG1 : CG0);
-    const int cb = COLP ? pass * PW0 : 0;
+    const int ng = RP * CG0;
+    const int cb = 0;
 #pragma unroll
     for (int k = 0; k < (PSRC ? PF : 0); ++k) {
       int trow, c0;
@@ -608,25 +579,7 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
 #pragma unroll 1
   for (int pass = 0; pass < NPASS; ++pass) {
     if (!W && (!EARLY || pass > 0)) prefetch(pass);  // (before the park: latency under the park + barrier)
-    if constexpr (COLP) {
-      // every wave: fragments [0, NHP) in pass 0, [NHP, NREP) in pass 1 (compile-time indices)
-      float* base = s_acc + (wm * WTM + 4 * g) * LDW + l16;
-      if (pass == 0) {
-#pragma unroll
-        for (int m = 0; m < MREP; ++m)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg)
-#pragma unroll
-            for (int n = 0; n < NHP; ++n) base[(m * 16 + reg) * LDW + n * 16] = acc[m][n][reg];
-      } else {
-#pragma unroll
-        for (int m = 0; m < MREP; ++m)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg)
-#pragma unroll
-            for (int n = NHP; n < NREP; ++n) base[(m * 16 + reg) * LDW + (n - NHP) * 16] = acc[m][n][reg];
-      }
-    } else if (wm * WTM >= pass * RP && wm * WTM < (pass + 1) * RP) {
+    if (wm * WTM >= pass * RP && wm * WTM < (pass + 1) * RP) {
       float* base = s_acc + (wm * WTM - pass * RP + 4 * g) * LDW + wn * WTN + l16;  // constant offsets below
 #pragma unroll
       for (int m = 0; m < MREP; ++m)
@@ -637,8 +590,8 @@ __global__ __launch_bounds__(512) void halo_kernel(const Grouped<HaloArgs, NG> G
     }
     EPI_BARRIER();
     if (pass == 0) TPG_TL_MARK(5);
-    const int ng = RP * ((COLP && pass) ? CG1 : CG0);
-    const int cb = COLP ? pass * PW0 : 0;  // first tile column of the pass
+    const int ng = RP * CG0;
+    const int cb = 0;  // first tile column of the pass
     if (W) {  // split-K partial slice rows (fp32, row stride Nout)
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
@@ -921,7 +874,8 @@ int launch_halo_group(const HaloArgs* a, int n, int dtype, int cfg, hipStream_t 
 // -------------------------------------------------------------- halo weight packing --
 // Wp[ks*ntaps + tap][ntile][BNL rows][4 chunks][EPC]: row r of N-tile nt is output
 // n' = nt*BN + r (zero when r >= BN or n' >= Nout); chunk' = chunk ^ hswz(r) holds
-// logical channels c = ks*KS + chunk*EPC + e of that tap.
+// logical channels c = ks*KS + chunk*EPC + e of that tap.  A paired last k-step (half) has
+// ceil(ntaps / 2) slices after the full ones (pack_halo_item).
 // One thread per 16-byte chunk, 32-bit index math (the packed image is < 2^31 elements).
 template <typename E>
 __global__ __launch_bounds__(256) void pack_halo_kernel(const PackArgs p, int nks, int bn, int bnl, int ntiles,
@@ -930,12 +884,12 @@ __global__ __launch_bounds__(256) void pack_halo_kernel(const PackArgs p, int nk
   if (idx < nchunks) pack_halo_item<E>(p, bn, bnl, ntiles, idx);
 }
 
-size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles) {
-  return (size_t)nks * ntaps * ntiles * halo_bnl(bn) * 64;
+size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles, int half) {
+  return (size_t)halo_steps(nks, ntaps, half) * ntiles * halo_bnl(bn) * 64;
 }
 
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s) {
-  const int nchunks = nks * a.ntaps * ntiles * halo_bnl(bn) * 4;
+  const int nchunks = halo_steps(nks, a.ntaps, a.half) * ntiles * halo_bnl(bn) * 4;
   const int blocks = (nchunks + 255) / 256;
   if (a.dtype == 2)
     hipLaunchKernelGGL(pack_halo_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, a, nks, bn, halo_bnl(bn), ntiles, nchunks);

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
             E o;
             if (XA) {
               const unsigned short x16 = (unsigned short)(e ? (xh >> 16) : (xh & 0xffffu));
-              o = (E)tpg_xa_grad(x, (float)__builtin_bit_cast(E, x16), p.xa_act, p.xa_slope, p.xa_segs, col + u);
+              o = (E)tpg_xa_grad(x, (float)__builtin_bit_cast(E, x16), p.xa_act, p.xa_slope);
             } else {
               o = (E)act_apply(x, p.act, p.slope);
             }
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const Grouped<EpiArgs, NG
       float x = v[u];
       if (p.bias) x += p.bias[p.bias_mod ? (col + u) % p.bias_mod : col + u];
       if (R) x += p.res_scale * ld_f(R + ro + u);
-      st_f(Y + yo + u, XA ? tpg_xa_grad(x, ld_f(XA + yo + u), p.xa_act, p.xa_slope, p.xa_segs, col + u)
+      st_f(Y + yo + u, XA ? tpg_xa_grad(x, ld_f(XA + yo + u), p.xa_act, p.xa_slope)
                           : act_apply(x, p.act, p.slope));
     }
   }

@@ -55,22 +55,8 @@ __device__ __forceinline__ float tpg_act_grad(float g, float y, int act, float s
   return g;
 }
 
-// per-channel-segment slopes of desc.in_act = TPG_ACT_CHANNEL (kernel arguments: no loads)
-struct XaSegs {
-  int nseg;
-  int end[4];
-  float slope[4];
-};
-
-// the input-gradient epilogue's producer act' (desc.in_act): a segment slope when nseg > 0
-__device__ __forceinline__ float tpg_xa_grad(float g, float x, int act, float slope, const XaSegs& sg, int c) {
-  if (sg.nseg > 0) {
-    float s = sg.slope[3];
-    s = c < sg.end[2] ? sg.slope[2] : s;
-    s = c < sg.end[1] ? sg.slope[1] : s;
-    s = c < sg.end[0] ? sg.slope[0] : s;
-    return x > 0.f ? g : g * s;
-  }
+// the input-gradient epilogue's producer act' (desc.in_act)
+__device__ __forceinline__ float tpg_xa_grad(float g, float x, int act, float slope) {
   return tpg_act_grad(g, x, act, slope);
 }
 
@@ -273,6 +259,7 @@ struct PackArgs {
   int nmode, cmode;
   int comp_kw, comp_c;        // composite decode: idx = (r*kw + s)*comp_c + ch
   int dtype;
+  int hnks, half;             // halo layout: k-steps, and whether the last one is paired (HaloArgs.half)
   int8_t tr[TPG_MAX_TAPS], ts[TPG_MAX_TAPS];
 };
 
@@ -344,12 +331,25 @@ __device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bn
   rr /= bnl;
   const int nt = rr % ntiles;
   rr /= ntiles;
-  const int tap = rr % p.ntaps;
-  const int ks = rr / p.ntaps;
-  const int c0 = ks * ROW + (pchunk ^ pack_hswz(r)) * EPC;
+  // step rr: k-step rr / ntaps, tap rr % ntaps; past the full k-steps of a paired image (half:
+  // the last k-step holds <= 16 live channels) step j carries taps 2j (logical chunks 0, 1) and
+  // 2j + 1 (chunks 2, 3), channels 0..15 of that k-step each (tpg_halo.hip compute)
+  const int lc = pchunk ^ pack_hswz(r);
+  const int nfull = (p.half ? p.hnks - 1 : p.hnks) * p.ntaps;
+  int tap, c0;
+  bool tap_ok = true;
+  if (rr < nfull) {
+    tap = rr % p.ntaps;
+    c0 = (rr / p.ntaps) * ROW + lc * EPC;
+  } else {
+    tap = 2 * (rr - nfull) + (lc >> 1);
+    c0 = (p.hnks - 1) * ROW + (lc & 1) * EPC;
+    tap_ok = tap < p.ntaps;
+    if (!tap_ok) tap = 0;
+  }
   const int np = nt * bn + r;
   union { uint4 u; E e[EPC]; } o;
-  const bool row_ok = r < bn && np < p.Nreal;
+  const bool row_ok = r < bn && np < p.Nreal && tap_ok;
   const int tr = p.tr[tap], ts = p.ts[tap];
   const int64_t base = (int64_t)tr * p.w_sr + (int64_t)ts * p.w_ss +
                        (p.nmode == 0 ? (int64_t)np * p.w_sa : (int64_t)np * p.w_sb);
@@ -374,21 +374,6 @@ __device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bn
 
 int launch_pack_many(const PackJob* jobs_dev, int n, int nblocks, hipStream_t s);
 
-// Adam fused with the packing of each parameter's owner image (tpg_adam_pack_run)
-constexpr int TPG_ADAM_RANGE_BLOCK = 4096;  // elements per block of a range job
-struct AdamPackJob {
-  PackJob pj;                 // owner: a halo-layout image with unit channel stride (pj.k.W in the params)
-  int kind;                   // 0: element range, 1: owner image
-  int64_t off, len;           // range: flat elements [off, off + len); owner: len = parameter chunks
-  int first_block, nblocks;
-};
-int launch_adam_pack(const AdamPackJob* jobs, int n, int nblocks, float* p, const float* g, float* m, float* v,
-                     float lr, float b1, float b2, float eps, float wd, const float* st, float gscale, hipStream_t s);
-int launch_adam_sched(float* st, float b1, float b2, int host_step, hipStream_t s);
-// dx[p][c] *= (x[p][c] > 0 ? 1 : slopes[c]) in place (desc.in_act TPG_ACT_CHANNEL, plans whose
-// epilogue cannot apply it)
-int launch_act_chan_inplace(int n, int c, int h, int w, const tpg_tensor& x, const tpg_tensor& dx, const XaSegs& sg,
-                            hipStream_t s);
 
 struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [+ res])
   const float* ws;
@@ -410,7 +395,6 @@ struct EpiArgs {               // split-K finalize: Y = act(sum_z ws[z] + bias [
   const void* XA;
   int xa_act;
   float xa_slope;
-  XaSegs xa_segs;             // per-channel-segment slopes (TPG_ACT_CHANNEL: nseg > 0)
 };
 
 // ---------------------------------------------------------------- halo direct conv ----
@@ -423,6 +407,7 @@ struct HaloArgs {
   int A_H, A_W, C;
   int nks;                    // 64-byte channel steps = ceil(C / KS)
   int ntaps;
+  int half;                   // 16-bit, C % 32 in 1..16: the last k-step runs two taps per MFMA (paired steps)
   int dymin, dxmin, HH, HW;   // halo of one sub-tile = HH x HW pixels
   int pad_mode, vec_ok;        // vec_ok: 16-byte loads of whole chunks stay inside each pixel row
   int pw;                     // > 0: one-tap problem on the pointwise GEMM kernel, tile config (tpg_pw.hip)
@@ -459,7 +444,6 @@ struct HaloArgs {
   const void* XA;
   int xa_act;
   float xa_slope;
-  XaSegs xa_segs;             // TPG_ACT_CHANNEL: never set for halo plans (run_probs; the pointwise epilogue reads it)
   // the prologue's index math by multiply-shift (each runtime division was ~25 VALU; the
   // small-map blocks spent ~1-2 us of a ~5 us prologue on them): HH*HW, HW, tiles_h*tiles_w,
   // tiles_w, TH*TW, TW
@@ -552,6 +536,11 @@ int launch_l1_set(int nseg, const tpg_l1_seg* segs, float* part, const float* go
 int pw_tile_bm(int cfg);
 int pw_tile_bn(int cfg);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);
-size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles);
+// pipeline steps of a halo problem (= weight slices of its packed image): ntaps per k-step, the
+// last k-step paired (ceil(ntaps / 2)) when half
+__host__ __device__ inline int halo_steps(int nks, int ntaps, int half) {
+  return half ? (nks - 1) * ntaps + (ntaps + 1) / 2 : nks * ntaps;
+}
+size_t halo_wp_bytes(int nks, int ntaps, int bn, int ntiles, int half);
 
 }  // namespace tpg

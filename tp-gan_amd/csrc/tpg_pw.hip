@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void pw_kernel(const HaloArgs p) {
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        o.e[e] = (E)tpg_xa_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope, p.xa_segs, min(col0 + e, p.Nout - 1));
+        o.e[e] = (E)tpg_xa_grad(v[e], (float)xx.e[e], p.xa_act, p.xa_slope);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o.e[e] = (E)tpg_act(v[e], p.act, p.slope);

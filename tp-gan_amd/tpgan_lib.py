@@ -18,7 +18,7 @@ if os.environ.get("TPG_LIB_PATH"):  # A/B builds of the same library (tools/ onl
     LIB_PATH = os.environ["TPG_LIB_PATH"]
 
 TPG_F32, TPG_BF16, TPG_F16 = 0, 1, 2
-ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6, ACT_CHANNEL = 0, 1, 2, 3, 4
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3
 PAD_ZERO, PAD_REFLECT = 0, 1
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
 
@@ -34,8 +34,7 @@ class ConvDesc(ctypes.Structure):
         "pad_t", "pad_b", "pad_l", "pad_r", "pad_mode", "transposed", "dtype", "act")] + [
         ("slope", ctypes.c_float), ("res_scale", ctypes.c_float), ("ksplit", ctypes.c_int32),
         ("algo", ctypes.c_int32), ("flags", ctypes.c_int32), ("data_ksplit", ctypes.c_int32),
-        ("data_algo", ctypes.c_int32), ("in_act", ctypes.c_int32), ("in_slope", ctypes.c_float),
-        ("in_nseg", ctypes.c_int32), ("in_seg_end", ctypes.c_int32 * 4), ("in_seg_slope", ctypes.c_float * 4)]
+        ("data_algo", ctypes.c_int32), ("in_act", ctypes.c_int32), ("in_slope", ctypes.c_float)]
 
 
 class L1Seg(ctypes.Structure):  # tpg_l1_seg
@@ -102,14 +101,6 @@ EXPORTS = {
     "tpg_conv2d_pack_jobs": (ctypes.c_int32, [ctypes.POINTER(ConvDesc), ctypes.c_int32, TpgTensor, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_int32]),
     "tpg_pack_prepare": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int32]),
-    "tpg_adam_pack_job_bytes": (ctypes.c_size_t, []),
-    "tpg_adam_pack_owner_ok": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int64]),
-    "tpg_adam_pack_jobs": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
-                                            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
-    "tpg_adam_pack_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
-                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
-                                           ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                                           ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_pack_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p]),
     "tpg_landmark_boxes": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),

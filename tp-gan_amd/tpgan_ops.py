@@ -18,7 +18,7 @@ import weakref
 
 import torch
 
-from tpgan_lib import (ACT_CHANNEL, ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_DX_ACCUM, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
+from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_DX_ACCUM, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
                        PAD_REFLECT,
                        PAD_ZERO, TPG_BF16, TPG_F32, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load,
                        stream_ptr, tt)
@@ -817,18 +817,13 @@ def _conv_act_backward_fused(ctx, gy, keep=None):
                (ctx.link_dx is None or bool(d.flags & FLAG_DX_ACCUM)))
     d.act = act_eff
     if fuse_in:
-        if isinstance(tok_in, CatToken):  # per-channel-segment slopes of the concatenated producers
-            d.in_act, d.in_nseg = ACT_CHANNEL, len(tok_in.slopes)
-            for k, (end, sl) in enumerate(tok_in.slopes):
-                d.in_seg_end[k], d.in_seg_slope[k] = end, sl
-        else:
-            d.in_act, d.in_slope = tok_in.act, tok_in.slope
+        d.in_act, d.in_slope = tok_in.act, tok_in.slope
     try:
         out = _conv_act_backward_fused_body(ctx, gy, keep, lib, x, weight, y, d, dtype, n, cout, oh, ow, need_dx, need_dw,
                                             g_is_gy, g, dbias, fused_b, acc, dx, act_eff)
     finally:
         d.act = ctx.act
-        d.in_act, d.in_slope, d.in_nseg = ACT_NONE, 0.0, 0
+        d.in_act, d.in_slope = ACT_NONE, 0.0
     if fuse_in and out[0] is not None:
         tok_in.take(out[0])
     return out
@@ -1228,61 +1223,10 @@ class ActToken(object):
         self.pre = dx
 
 
-class CatToken(object):
-    """ActToken of a channel concat (tpgan_ops.cat; D_and_G_model.py:309-325 torch.cat of the
-    decoder's upsample and add_conv_and_deconv outputs): each slice keeps its producer's token
-    (or none: slope 1), and the consumer's epilogue applies the per-channel slopes
-    (desc.in_act = TPG_ACT_CHANNEL).  The producers receive their slice of the concat's
-    gradient (_Cat.backward: channel views), which is the slice of the consumer's dx."""
-    __slots__ = ("segs", "slopes", "y")
-
-    def __init__(self, segs, slopes):
-        # segs: [(c0, c1, ActToken)]; slopes: [(channel end, slope)] runs of equal slope (<= 4)
-        self.segs, self.slopes, self.y = segs, slopes, None
-
-    def take(self, dx):
-        for c0, c1, tok in self.segs:
-            tok.take(dx[:, c0:c1])
-
-
-# Concat links are built and tested but off: measured SLOWER on the train step (same-box A/B,
-# 33.40 vs 32.87 ms/step with them off): the producers then read their gradient as a channel
-# slice of the concat's (upsample_128: 64 of 208 channels per pixel, deconv_128: 8 of 75), so
-# their weight / input-gradient kernels fetch 3-8x the bytes the dense act_bwd output cost, and
-# add_128's residual block accumulates into a slice whose strides differ from its input's (the
-# epilogue cannot take act' there: an extra pass).  The slices that are a large share of their
-# concat would gain a few us each.
-CAT_LINK = {"enabled": False}
-
-
-def _cat_token(xs, act_in_ok, out):
-    """The CatToken of cat(xs) when some input carries an ActToken its caller declared consumed
-    by this concat alone (act_in_ok[i]); None otherwise."""
-    if not (ACT_LINK["enabled"] and CAT_LINK["enabled"] and torch.is_grad_enabled()) or not act_in_ok:
-        return None
-    dt = get_compute_dtype()
-    segs, slopes, off = [], [], 0
-    for x, ok in zip(xs, act_in_ok):
-        c = x.shape[1]
-        tok = getattr(x, "_tpg_act_tok", None) if ok else None
-        if (isinstance(tok, ActToken) and tok.y is not None and tok.y() is x and x.dtype == dt and
-                tok.act in (ACT_LEAKY, ACT_RELU)):
-            segs.append((off, off + c, tok))
-            slopes += [tok.slope if tok.act == ACT_LEAKY else 0.0] * c
-        else:
-            slopes += [1.0] * c  # (no activation to apply: these inputs mask their own gradient, if any)
-        off += c
-    if not segs:
-        return None
-    runs = []  # (channel end, slope) of each run of equal slope
-    for c, sl in enumerate(slopes):
-        if runs and runs[-1][1] == sl:
-            runs[-1][0] = c + 1
-        else:
-            runs.append([c + 1, sl])
-    if len(runs) > 4:  # (desc.in_seg_*: four segments)
-        return None
-    return CatToken(segs, [tuple(r) for r in runs])
+# (Concat links -- a CatToken carrying per-channel-segment slopes of a concat's producers into
+# the consuming conv's epilogue, desc.in_act = TPG_ACT_CHANNEL -- were built in round 5 and
+# removed in round 6: measured slower on the train step, 33.40 vs 32.87 ms/step, since the
+# producers then read their gradients as strided channel slices of the concat's.)
 
 
 ACT_LINK = {"enabled": True}  # (A/B, tests: off = every conv masks its own gradient)
@@ -1587,16 +1531,9 @@ class _Cat(torch.autograd.Function):
         return tuple(outs)
 
 
-def cat(xs, act_in_ok=None):
-    """torch.cat(xs, 1) into one channels-last buffer.  act_in_ok: per input, the caller's
-    promise that the input is consumed by this concat alone -- its producer's activation
-    backward may then run in the epilogue of the concat's consuming conv (CatToken)."""
-    out = _Cat.apply(*xs)
-    tok = _cat_token(xs, act_in_ok, out) if act_in_ok is not None else None
-    if tok is not None:
-        tok.y = weakref.ref(out)
-        out._tpg_act_tok = tok
-    return out
+def cat(xs):
+    """torch.cat(xs, 1) into one channels-last buffer."""
+    return _Cat.apply(*xs)
 
 
 # ---- fused G-step image losses (tpg_losses.hip; tpgan_train._g_losses): one partial-sum and one
@@ -1832,92 +1769,6 @@ def repack_range(flat, off, n, epoch):
         check(lib.tpg_pack_run(dev.data_ptr(), nj, nblocks, stream_ptr()))
     for e in entries:
         e.epoch = epoch
-
-
-# Adam fused with the weight repack (tpg_adam_pack_run): each conv parameter whose pre-packed
-# images include one with unit channel stride covering it exactly once (the forward image of a
-# channels-last Conv2d weight, the input-gradient image of a ConvTranspose2d's) has that image
-# written by the update itself -- one read of the fp32 master instead of two; every other flat
-# element is updated by range jobs of the same launch, and the remaining images are re-packed
-# from the updated master afterwards (one pack_many launch).  Bit-identical to tpg_adam + repack
-# (tests/test_gpu_train.py), but measured SLOWER (tools/bench_opt.py, G: fused 1.08 + rest pack
-# 0.34 ms against Adam 0.65 + pack 0.51; the step +0.75 ms before the half-chunk lanes): the
-# owner images' share of the pack is only 0.17 ms, less than the fused kernel loses against the
-# plain streaming update.  Off by default (measured, not adopted).
-FUSED_ADAM_PACK = {"enabled": False}
-
-
-def _adam_pack_table(flat):
-    """(device jobs, n, nblocks, rest device table, rest n, rest nblocks, entries) for flat's
-    current pack entries, cached until they change."""
-    cache = getattr(flat, "adam_pack_table", None)
-    if cache is not None and cache[0] == flat.pack_version:
-        return cache[1]
-    lib = load()
-    pjb = lib.tpg_pack_job_bytes()
-    base = flat.data.data_ptr()
-    entries = [e for e in flat.pack_entries.values() if e is not None and e.njobs]
-    # param index by its first element
-    starts = {off: i for i, off in enumerate(flat.offsets)}
-    owners, owned, rest = [], {}, []
-    for k, e in flat.pack_entries.items():
-        if e is None or not e.njobs:
-            continue
-        pi = starts.get((k[2] - base) // 4) if (k[2] - base) % 4 == 0 else None
-        ok = (pi is not None and pi not in owned and e.njobs == 1 and
-              lib.tpg_adam_pack_owner_ok(e.jobs[:pjb], flat.params[pi].numel()) == 1)
-        if ok:
-            owned[pi] = e
-            owners.append(e.jobs[:pjb])
-        else:
-            rest.append(e)
-    # element ranges of everything not owned, in flat order
-    ranges, cur = [], None
-    for i in sorted(range(len(flat.params)), key=lambda j: flat.offsets[j]):
-        if i in owned:
-            continue
-        off, n = flat.offsets[i], flat.params[i].numel()
-        if cur is not None and cur[0] + cur[1] == off:
-            cur[1] += n
-        else:
-            if cur is not None:
-                ranges.append(cur)
-            cur = [off, n]
-    if cur is not None:
-        ranges.append(cur)
-    ajb = lib.tpg_adam_pack_job_bytes()
-    nmax = len(owners) + len(ranges)
-    out = ctypes.create_string_buffer(ajb * max(nmax, 1))
-    own_raw = ctypes.create_string_buffer(b"".join(owners), max(len(owners) * pjb, 1))
-    rng = (ctypes.c_int64 * max(2 * len(ranges), 1))(*[v for r in ranges for v in r])
-    nb = ctypes.c_int64(0)
-    n = lib.tpg_adam_pack_jobs(own_raw, len(owners), rng, len(ranges), out, nmax, ctypes.byref(nb))
-    check(n if n < 0 else 0)
-    dev = torch.frombuffer(bytearray(out.raw[:ajb * n]), dtype=torch.uint8).to(flat.data.device) if n else None
-    rdev, rn, rnb = None, 0, 0
-    if rest:
-        raw = b"".join(e.jobs for e in rest)
-        rn = sum(e.njobs for e in rest)
-        host = ctypes.create_string_buffer(raw, len(raw))
-        rnb = lib.tpg_pack_prepare(host, rn)
-        rdev = torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(flat.data.device)
-    tab = (dev, n, int(nb.value), rdev, rn, rnb, entries, len(owners))
-    flat.adam_pack_table = (flat.pack_version, tab)
-    return tab
-
-
-def adam_pack(flat, lr, beta1, beta2, eps, weight_decay, state, step=0, grad_scale=1.0):
-    """adam_step over the whole flat buffer + repack(flat), as tpg_adam_pack_run (+ one
-    tpg_pack_run for the images no update owns).  Marks every image packed at flat.epoch."""
-    lib = load()
-    dev, n, nb, rdev, rn, rnb, entries, _ = _adam_pack_table(flat)
-    check(lib.tpg_adam_pack_run(dev.data_ptr() if dev is not None else None, n, nb, flat.data.data_ptr(),
-                                flat.grad.data_ptr(), flat.exp_avg.data_ptr(), flat.exp_avg_sq.data_ptr(), lr, beta1,
-                                beta2, eps, weight_decay, int(step), grad_scale, state.data_ptr(), stream_ptr()))
-    if rn:
-        check(lib.tpg_pack_run(rdev.data_ptr(), rn, rnb, stream_ptr()))
-    for e in entries:
-        e.epoch = flat.epoch
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, state, step=0, grad_scale=1.0):

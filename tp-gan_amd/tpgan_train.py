@@ -110,17 +110,16 @@ class FlatParams:
         self.step += 1
         if check_finite:
             tpgan_ops.grad_check(self.grad, self.adam_state)
-        fused = tpgan_ops.FUSED_ADAM_PACK["enabled"] and self.data.is_cuda and tpgan_ops.PACK["enabled"]
-        if not fused:
-            tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
-                                weight_decay, self.adam_state, 0, grad_scale)
+        # (Adam fused with the weight-image repack was built in round 5 and removed in round 6:
+        # bit-identical but slower, G 1.084 + 0.341 ms against 0.652 + 0.509 ms isolated --
+        # the images' 16-byte chunks gather 8 channels from 8 master rows, so one of the two
+        # streams scatters whichever order the fused kernel walks)
+        tpgan_ops.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
+                            weight_decay, self.adam_state, 0, grad_scale)
         if check_finite:  # (on the device: no synchronisation; skipped_steps() reads it)
             self.skipped.add_(self.adam_state[3].ne(0).float())
         self.epoch += 1
-        if fused:  # (the update and the weight images in one launch; the skip check is the kernel's)
-            tpgan_ops.adam_pack(self, lr, betas[0], betas[1], eps, weight_decay, self.adam_state, 0, grad_scale)
-        else:
-            tpgan_ops.repack(self)
+        tpgan_ops.repack(self)
 
     def skipped_steps(self):
         """Updates skipped for non-finite gradients so far (synchronises).  A run whose static
@@ -463,7 +462,7 @@ FUSED_LOSSES = {"enabled": True}
 # stream crashed in the first replay of a later whole-step capture (r05aj-r05al; reusing the
 # stream, r05aq, it does not).  Not inside capture() ("in_capture"): hipStreamEndCapture
 # crashed with the fork in the graph (r05ar).  False: everything on the step's stream.
-IDENTITY_STREAM = {"enabled": True, "in_capture": False}
+IDENTITY_STREAM = {"enabled": True, "in_capture": False, "own_stream": False}
 
 
 def total_variation(x):
@@ -705,7 +704,8 @@ class TPGANTrainer:
                 (not self._graph_setup or IDENTITY_STREAM.get("in_capture", False))):
             main = torch.cuda.current_stream()
             # (the real-image features' stream: they ran in phase A, so the two never overlap)
-            id_st = tpgan_ops.side_streams(fake.device, 1, "identity")[0]
+            id_st = tpgan_ops.side_streams(fake.device, 1, "identity_fork" if IDENTITY_STREAM["own_stream"]
+                                           else "identity")[0]
             id_st.wait_stream(main)
             with torch.cuda.stream(id_st):
                 l_ip = self._identity_loss(fake, front)
@@ -933,9 +933,6 @@ class TPGANTrainer:
         # steps updated G bucket by bucket and never needed it); the images are re-packed unchanged
         tpgan_ops.repack(self.fG)
         tpgan_ops.repack(self.fD)
-        if tpgan_ops.FUSED_ADAM_PACK["enabled"]:
-            for f in (self.fG, self.fD):  # (the fused update's job tables: host -> device copies)
-                tpgan_ops._adam_pack_table(f)
         torch.cuda.synchronize()
         self._capturing = True  # graph replays reduce G in one call between phases
         self._segmented = bool(segmented)
