@@ -1014,48 +1014,63 @@ class _ActMask(torch.autograd.Function):
         return _ActMask.apply(dg, y, ctx.act, ctx.slope), None, None, None
 
 
+# (wp: the FlatParams parameter w is (a view of), when w is a layer's weight -- its pre-packed
+# images then serve these launches as they serve the first-order ones, instead of a pack launch
+# per call; None for a weight GRADIENT in the weight slot of the second-order terms)
 class _ConvFwdPlain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, d):
+    def forward(ctx, x, w, d, wp=None):
         lib = load()
         x = _fix_c1(to_cl(x, dtype_from_code(d.dtype)))
         y = new_act(d.n, d.out_c, d.out_h, d.out_w, x.dtype, x.device)
         ws = _ws(lib, d, OP_FWD, x.device)
         FLOPS["fwd"] += _conv_flops(d)
-        check(lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(w.float()), None, TpgTensor(), tt(_fix_c1(y)),
-                                 ws.data_ptr(), ws.numel(), stream_ptr()))
+        wv = w.float()
+        pk = _packed_weight(wp, d, OP_FWD, wv) if wp is not None else None
+        _run_maybe_packed(
+            lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), _packed_tt(pk), None, TpgTensor(), tt(_fix_c1(y)),
+                                       ws.data_ptr(), ws.numel(), stream_ptr()),
+            lambda: lib.tpg_conv2d_fwd(ctypes.byref(d), tt(x), tt(wv), None, TpgTensor(), tt(_fix_c1(y)),
+                                       ws.data_ptr(), ws.numel(), stream_ptr()), d, pk)
         ctx.save_for_backward(x, w)
         ctx.d = d
+        ctx.wp = wp
         return _fix_c1(y)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = _ConvDgrad.apply(dy, w, ctx.d) if ctx.needs_input_grad[0] else None
+        dx = _ConvDgrad.apply(dy, w, ctx.d, ctx.wp) if ctx.needs_input_grad[0] else None
         dw = _ConvWgrad.apply(x, dy, ctx.d) if ctx.needs_input_grad[1] else None
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class _ConvDgrad(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, g, w, d):
+    def forward(ctx, g, w, d, wp=None):
         lib = load()
         g = _fix_c1(to_cl(g, dtype_from_code(d.dtype)))
         dx = new_act(d.n, d.in_c, d.in_h, d.in_w, g.dtype, g.device)
         ws = _ws(lib, d, OP_BWD_DATA, g.device)
         FLOPS["dgrad"] += _conv_flops(d)
-        check(lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(w.float()), tt(_fix_c1(dx)), ws.data_ptr(),
-                                      ws.numel(), stream_ptr()))
+        wv = w.float()
+        pk = _packed_weight(wp, d, OP_BWD_DATA, wv) if wp is not None else None
+        _run_maybe_packed(
+            lambda: lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), _packed_tt(pk), tt(_fix_c1(dx)), ws.data_ptr(),
+                                            ws.numel(), stream_ptr()),
+            lambda: lib.tpg_conv2d_bwd_data(ctypes.byref(d), tt(g), tt(wv), tt(_fix_c1(dx)), ws.data_ptr(),
+                                            ws.numel(), stream_ptr()), d, pk)
         ctx.save_for_backward(g, w)
         ctx.d = d
+        ctx.wp = wp
         return _fix_c1(dx)
 
     @staticmethod
     def backward(ctx, ddx):
         g, w = ctx.saved_tensors
-        dg = _ConvFwdPlain.apply(ddx, w, ctx.d) if ctx.needs_input_grad[0] else None
+        dg = _ConvFwdPlain.apply(ddx, w, ctx.d, ctx.wp) if ctx.needs_input_grad[0] else None
         dw = _ConvWgrad.apply(ddx, g, ctx.d) if ctx.needs_input_grad[1] else None
-        return dg, dw, None
+        return dg, dw, None, None
 
 
 class _ConvWgrad(torch.autograd.Function):
@@ -1096,7 +1111,7 @@ def _conv_act_backward_graph(ctx, gy):
     g = _ActMask.apply(gy, y, ctx.d.act, ctx.d.slope)
     dx = dw = dbias = dres = None
     if ctx.needs_input_grad[0]:
-        dx = _ConvDgrad.apply(g, weight, d)
+        dx = _ConvDgrad.apply(g, weight, d, wp)
         if dx.dtype != ctx.in_dtype:
             dx = dx.to(ctx.in_dtype)
     if ctx.needs_input_grad[1]:
