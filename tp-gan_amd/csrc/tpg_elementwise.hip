@@ -50,19 +50,35 @@ __device__ __forceinline__ void pack_halo_block_t(const PackArgs& p, int bn, int
   const int r0 = lb * 64 - rr * bnl;
   const int nt = rr % ntiles;
   rr /= ntiles;
-  const int tap = rr % p.ntaps;
-  const int ks = rr / p.ntaps;
-  const int64_t tapoff = (int64_t)p.tr[tap] * p.w_sr + (int64_t)p.ts[tap] * p.w_ss;
+  // step rr as in pack_halo_item: a full k-step's tap, or (paired last k-step) taps 2j (logical
+  // channels 0..15 of the row) and 2j + 1 (16..31), channels 0..15 of that k-step each; the
+  // thread's quarter of the row (t >> 6) lies in one of the two halves
+  const int nfull = (p.half ? p.hnks - 1 : p.hnks) * p.ntaps;
+  const bool paired = rr >= nfull;
+  const int q = t >> 6;
+  int tap, ks, cbase;
+  if (!paired) {
+    tap = rr % p.ntaps;
+    ks = rr / p.ntaps;
+    cbase = ks * ROW + q * (ROW / 4);
+  } else {
+    tap = 2 * (rr - nfull) + (q >> 1);
+    ks = p.hnks - 1;
+    cbase = ks * ROW + (q & 1) * (ROW / 4);
+  }
+  const bool tap_ok = tap < p.ntaps;
+  const int tp = tap_ok ? tap : 0;
+  const int64_t tapoff = (int64_t)p.tr[tp] * p.w_sr + (int64_t)p.ts[tp] * p.w_ss;
   {
     const int rl = t & 63;
     const int r = r0 + rl;
     const int np = nt * bn + r;
-    const bool row_ok = r < bn && np < p.Nreal;
+    const bool row_ok = r < bn && np < p.Nreal && tap_ok;
     const float* src = p.W + tapoff + np;
 #pragma unroll
     for (int e = 0; e < ROW / 4; ++e) {
-      const int cl = (t >> 6) * (ROW / 4) + e;
-      const int c = ks * ROW + cl;
+      const int cl = q * (ROW / 4) + e;
+      const int c = cbase + e;
       tile[cl][rl] = (row_ok && c < p.Creal) ? src[(int64_t)c * p.w_sa] : 0.f;
     }
   }
