@@ -462,7 +462,7 @@ FUSED_LOSSES = {"enabled": True}
 # stream crashed in the first replay of a later whole-step capture (r05aj-r05al; reusing the
 # stream, r05aq, it does not).  Not inside capture() ("in_capture"): hipStreamEndCapture
 # crashed with the fork in the graph (r05ar).  False: everything on the step's stream.
-IDENTITY_STREAM = {"enabled": True, "in_capture": False, "own_stream": False}
+IDENTITY_STREAM = {"enabled": True, "in_capture": True, "own_stream": False}
 
 # D(real) beside G's forward (one process): the critic's pass on the real images -- forward and
 # the backward of -mean D(real) into fD.grad -- depends only on D's weights, not on this step's
