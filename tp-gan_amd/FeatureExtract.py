@@ -95,9 +95,13 @@ class IdentityPreservingLoss(nn.Module):
             if pre is not None:
                 st, fr = pre
                 main = torch.cuda.current_stream()
-                main.wait_stream(st)
-                for t in fr:
-                    t.record_stream(main)
+                # (the identity fork of tpgan_train runs this on the features' own stream: no
+                # event wait of a stream on itself -- inside a graph capture that self-edge
+                # crashed hipStreamEndCapture, gpurun r05ar / r06e)
+                if main != st:
+                    main.wait_stream(st)
+                    for t in fr:
+                        t.record_stream(main)
             else:
                 with torch.no_grad():
                     fr = self.extractor.extract_features(real)

@@ -464,14 +464,6 @@ FUSED_LOSSES = {"enabled": True}
 # crashed with the fork in the graph (r05ar).  False: everything on the step's stream.
 IDENTITY_STREAM = {"enabled": True, "in_capture": True, "own_stream": False}
 
-# D(real) beside G's forward (one process): the critic's pass on the real images -- forward and
-# the backward of -mean D(real) into fD.grad -- depends only on D's weights, not on this step's
-# G, so it runs on a side stream planned for a share of the chip while G's forward runs (its
-# small-map encoder / decoder layers leave most CUs idle); phase A then runs D on the B fake
-# images alone and adds their gradient (the real_ahead split of the 2B critic batch, SURVEY.md
-# §8e, inside one step).  False: one 2B critic batch after G's forward.
-REAL_SIDE = {"enabled": True}
-
 
 def total_variation(x):
     return (x[:, :, 1:, :] - x[:, :, :-1, :]).abs().mean() + (x[:, :, :, 1:] - x[:, :, :, :-1]).abs().mean()
@@ -620,18 +612,6 @@ class TPGANTrainer:
             self.fD.zero_grad()
         else:
             self.real_ahead_used += 1
-        real_side = None
-        if (d_real_pre is None and REAL_SIDE["enabled"] and self.world == 1 and not self.gp and
-                tpgan_ops.MULTISTREAM and b["frontal"].is_cuda):
-            main = torch.cuda.current_stream()
-            st = tpgan_ops.side_streams(b["frontal"].device, 1, "dreal")[0]
-            st.wait_stream(main)  # (after fD.zero_grad)
-            with torch.cuda.stream(st), tpgan_ops.concurrent(), tpgan_ops.roctx_range("D-real-side"), \
-                    tpgan_ops.compute_dtype(self.dtype):
-                d_real_s = self.D(tpgan_ops.to_cl(b["frontal"], self.dtype)).float()
-                loss_r = -d_real_s.mean()
-                (loss_r * self.loss_scale if self.loss_scale != 1.0 else loss_r).backward()
-            real_side = (st, d_real_s.detach())
         # the identity loss's real-image features run on a side stream under G's forward
         # (not while phase A is captured as a graph of its own: the fork would stay unjoined
         # at the end of that capture, and phase B's graph would wait on work of another graph)
@@ -646,12 +626,6 @@ class TPGANTrainer:
             B = fake.shape[0]
             with tpgan_ops.roctx_range("D-step"):
                 real = tpgan_ops.to_cl(b["frontal"], self.dtype)
-                if real_side is not None:
-                    # (D(real)'s gradient is in fD.grad once the side stream is joined; D(fake)'s
-                    # backward adds to it)
-                    torch.cuda.current_stream().wait_stream(real_side[0])
-                    d_real_pre = (None, None, real_side[1])
-                    real_side[1].record_stream(torch.cuda.current_stream())
                 if d_real_pre is None:
                     # ---- D-step (critic on real and detached fake as one 2B batch)
                     d_both = D(torch.cat([real, fake.detach()], 0)).float()
