@@ -277,6 +277,10 @@ class FeaturePredict(nn.Module):
         return tpgan_ops.linear(x, self.fc.weight, self.fc.bias)
 
 
+# (A/B switch for the round-6 measurement of the fusers on the local stream; False: on the main stream)
+FUSER_SIDE = {"enabled": True}
+
+
 class Generator(nn.Module):
     """Four LocalPathways, three LocalFuser calls, the GlobalPathway and FeaturePredict;
     forward returns the reference's 8-tuple (D_and_G_model.py:350-407)."""
@@ -298,6 +302,7 @@ class Generator(nn.Module):
         paths = (self.local_pathway_left_eye, self.local_pathway_right_eye, self.local_pathway_nose,
                  self.local_pathway_mouth)
         patches = (left_eye, right_eye, nose, mouth)
+        fused = None
         if self._groupable is None:
             # lockstep grouping fuses conv + bias + activation layers only: with BatchNorm
             # (use_batchnorm=True, the reference default) group_forward would run the members
@@ -306,17 +311,24 @@ class Generator(nn.Module):
         if tpgan_ops.GROUP["enabled"] and I128.is_cuda and self._groupable:
             # the four local pathways in lockstep on one side stream (one grouped launch per
             # layer and kernel), concurrently with the global pathway's local-independent part
+            # The three LocalFuser calls run on that stream too, so their backward does: autograd
+            # replays a node on its forward's stream and takes ready nodes latest-created first,
+            # so a fuser on the main stream had its backward enqueued behind the WHOLE global
+            # backward -- and in a captured step the local pathways' backward then waited for it
+            # (gpurun r05ba trace: ~3 ms of local backward kernels at the end of the step).  On
+            # the side stream the fuser backward waits only for the gradients it consumes.
             main = torch.cuda.current_stream()
             st = tpgan_ops.side_streams(I128.device, 1, "local")[0] if tpgan_ops.MULTISTREAM else main
             st.wait_stream(main)
             with torch.cuda.stream(st), tpgan_ops.concurrent(tpgan_ops.MULTISTREAM):
                 outs = LocalPathway.forward_group(paths, patches)
+                if FUSER_SIDE["enabled"]:
+                    fused = self._fuse(outs, patches)
             enc = self.global_pathway.encode(I128, z)
             if st is not main:
                 main.wait_stream(st)
-                for img, feat in outs:
-                    img.record_stream(main)
-                    feat.record_stream(main)
+                for t in [t for o in outs for t in o] + list(fused or ()):
+                    t.record_stream(main)
         elif tpgan_ops.MULTISTREAM and I128.is_cuda:
             # The four local pathways (small maps: kernels that fill few CUs) run on their
             # own HIP streams, concurrently with the global pathway's local-independent part
@@ -337,17 +349,22 @@ class Generator(nn.Module):
         else:
             outs = [path(x) for path, x in zip(paths, patches)]
             enc = self.global_pathway.encode(I128, z)
-        ((left_eye_fake_image, left_eye_fake_feature), (right_eye_fake_image, right_eye_fake_feature),
-         (nose_fake_image, nose_fake_feature), (mouth_fake_image, mouth_fake_feature)) = outs
-        fused_local_feature = self.local_fuser(left_eye_fake_feature, right_eye_fake_feature, nose_fake_feature,
-                                               mouth_fake_feature)
-        fused_local_fake_image = self.local_fuser(left_eye_fake_image, right_eye_fake_image, nose_fake_image,
-                                                  mouth_fake_image)
-        fused_local_origin_4_part = self.local_fuser(left_eye, right_eye, nose, mouth)
+        if fused is None:
+            fused = self._fuse(outs, patches)
+        ((left_eye_fake_image, _), (right_eye_fake_image, _), (nose_fake_image, _), (mouth_fake_image, _)) = outs
+        fused_local_feature, fused_local_fake_image, fused_local_origin_4_part = fused
         I128_fake, encoder_feature = self.global_pathway.decode_128(enc, fused_local_fake_image, fused_local_feature)
         encoder_predict = self.feature_predict(encoder_feature, use_dropout)
         return (I128_fake, encoder_predict, fused_local_fake_image, left_eye_fake_image, right_eye_fake_image,
                 nose_fake_image, mouth_fake_image, fused_local_origin_4_part)
+
+
+    def _fuse(self, outs, patches):
+        """The three LocalFuser calls of the reference (D_and_G_model.py:395-398): the local
+        features, the local fake images, the real patches."""
+        ((le_img, le_feat), (re_img, re_feat), (no_img, no_feat), (mo_img, mo_feat)) = outs
+        return (self.local_fuser(le_feat, re_feat, no_feat, mo_feat), self.local_fuser(le_img, re_img, no_img, mo_img),
+                self.local_fuser(*patches))
 
 
 class Discriminator(nn.Module):
