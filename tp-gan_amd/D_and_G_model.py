@@ -277,8 +277,9 @@ class FeaturePredict(nn.Module):
         return tpgan_ops.linear(x, self.fc.weight, self.fc.bias)
 
 
-# (A/B switch for the round-6 measurement of the fusers on the local stream; False: on the main stream)
-FUSER_SIDE = {"enabled": True}
+# (A/B switch for the round-6 measurement: the local pathways created after the global encoder,
+# see Generator.forward; False: before it)
+LOCAL_LATE = {"enabled": True}
 
 
 class Generator(nn.Module):
@@ -311,23 +312,30 @@ class Generator(nn.Module):
         if tpgan_ops.GROUP["enabled"] and I128.is_cuda and self._groupable:
             # the four local pathways in lockstep on one side stream (one grouped launch per
             # layer and kernel), concurrently with the global pathway's local-independent part
-            # The three LocalFuser calls run on that stream too, so their backward does: autograd
-            # replays a node on its forward's stream and takes ready nodes latest-created first,
-            # so a fuser on the main stream had its backward enqueued behind the WHOLE global
-            # backward -- and in a captured step the local pathways' backward then waited for it
-            # (gpurun r05ba trace: ~3 ms of local backward kernels at the end of the step).  On
-            # the side stream the fuser backward waits only for the gradients it consumes.
+            # Backward order: autograd replays a node on its forward's stream and takes ready
+            # nodes latest-CREATED first.  Created before the global encoder, the local nodes
+            # (and the fusers, created on the main stream) had their backward enqueued behind the
+            # WHOLE global backward, and a captured step kept that order: ~3 ms of local
+            # backward kernels at the end of the step (gpurun r05ba / r06g traces).  So the fork
+            # point is taken first (st waits for the main stream as it is now), the global
+            # encoder is enqueued, and only then the local pathways and the three fusers on st:
+            # created after the encoder, their backward is enqueued as soon as the 128-px fusion
+            # hands them their gradients and runs beside the global decoder's backward.  (The
+            # GPU order of the forward is unchanged: st depends on the fork point only.)
             main = torch.cuda.current_stream()
             st = tpgan_ops.side_streams(I128.device, 1, "local")[0] if tpgan_ops.MULTISTREAM else main
             st.wait_stream(main)
+            late = LOCAL_LATE["enabled"] and st is not main
+            if late:
+                enc = self.global_pathway.encode(I128, z)
             with torch.cuda.stream(st), tpgan_ops.concurrent(tpgan_ops.MULTISTREAM):
                 outs = LocalPathway.forward_group(paths, patches)
-                if FUSER_SIDE["enabled"]:
-                    fused = self._fuse(outs, patches)
-            enc = self.global_pathway.encode(I128, z)
+                fused = self._fuse(outs, patches)
+            if not late:
+                enc = self.global_pathway.encode(I128, z)
             if st is not main:
                 main.wait_stream(st)
-                for t in [t for o in outs for t in o] + list(fused or ()):
+                for t in [t for o in outs for t in o] + list(fused):
                     t.record_stream(main)
         elif tpgan_ops.MULTISTREAM and I128.is_cuda:
             # The four local pathways (small maps: kernels that fill few CUs) run on their

@@ -697,9 +697,14 @@ class TPGANTrainer:
         fake, pred, fused_fake, le_f, re_f, no_f, mo_f, _ = self._st.pop("outs")
         front = b["frontal"]
         id_st, l_ip = None, None
-        # (eager training only: not in capture() -- its warm-up steps included -- since bench runs
-        # with this fork in the warm-up of a whole-step capture crashed the process, gpurun r05aj /
-        # r05ak, not yet understood; the captured step keeps the one-stream identity pass)
+        # The identity fork (in eager steps and, since round 6, inside graph captures: the
+        # round-5 crashes in hipStreamEndCapture came from an event wait of the features stream
+        # on itself, FeatureExtract.IdentityPreservingLoss).  Its fork point is taken here, where
+        # `fake` is ready, but its forward is enqueued after D's Adam and D(fake): its autograd
+        # nodes are then created later than D(fake)'s, so the backward (latest-created first)
+        # enqueues the identity input gradient on its stream before D(fake)'s on the main one,
+        # and neither waits for the other (enqueued the other way round, the captured step had
+        # the identity backward behind all of D(fake)'s).
         if (self.identity_fn is not None and IDENTITY_STREAM["enabled"] and fake.is_cuda and
                 tpgan_ops.MULTISTREAM and
                 (not self._graph_setup or IDENTITY_STREAM.get("in_capture", False))):
@@ -710,12 +715,6 @@ class TPGANTrainer:
             id_st.wait_stream(main)
             if self._capturing:
                 self.identity_forks_captured += 1
-            with torch.cuda.stream(id_st):
-                l_ip = self._identity_loss(fake, front)
-        elif self.identity_fn is not None:
-            # (the same point of the autograd graph as the side-stream form: the gradients at
-            # `fake` are then summed in the same order, and the two forms are bit-identical)
-            l_ip = self._identity_loss(fake, front)
         with tpgan_ops.compute_dtype(self.dtype):
             self.fD.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
                          check_finite=self.loss_scale != 1.0)
@@ -723,6 +722,13 @@ class TPGANTrainer:
             set_requires_grad(D.parameters(), False)
             d_gen = D(fake).float()
             set_requires_grad(D.parameters(), True)
+        if id_st is not None:
+            with torch.cuda.stream(id_st):
+                l_ip = self._identity_loss(fake, front)
+        elif self.identity_fn is not None:
+            # (the same point of the autograd graph as the side-stream form: the gradients at
+            # `fake` are then summed in the same order, and the two forms are bit-identical)
+            l_ip = self._identity_loss(fake, front)
         args = (fake, le_f, re_f, no_f, mo_f, d_gen, pred, front, b["frontal_left_eye"], b["frontal_right_eye"],
                 b["frontal_nose"], b["frontal_mouth"], b["label"])
         loss_G = self._g_losses(*args)
