@@ -277,11 +277,6 @@ class FeaturePredict(nn.Module):
         return tpgan_ops.linear(x, self.fc.weight, self.fc.bias)
 
 
-# (A/B switch for the round-6 measurement: the local pathways created after the global encoder,
-# see Generator.forward; False: before it)
-LOCAL_LATE = {"enabled": True}
-
-
 class Generator(nn.Module):
     """Four LocalPathways, three LocalFuser calls, the GlobalPathway and FeaturePredict;
     forward returns the reference's 8-tuple (D_and_G_model.py:350-407)."""
@@ -312,27 +307,20 @@ class Generator(nn.Module):
         if tpgan_ops.GROUP["enabled"] and I128.is_cuda and self._groupable:
             # the four local pathways in lockstep on one side stream (one grouped launch per
             # layer and kernel), concurrently with the global pathway's local-independent part
-            # Backward order: autograd replays a node on its forward's stream and takes ready
-            # nodes latest-CREATED first.  Created before the global encoder, the local nodes
-            # (and the fusers, created on the main stream) had their backward enqueued behind the
-            # WHOLE global backward, and a captured step kept that order: ~3 ms of local
-            # backward kernels at the end of the step (gpurun r05ba / r06g traces).  So the fork
-            # point is taken first (st waits for the main stream as it is now), the global
-            # encoder is enqueued, and only then the local pathways and the three fusers on st:
-            # created after the encoder, their backward is enqueued as soon as the 128-px fusion
-            # hands them their gradients and runs beside the global decoder's backward.  (The
-            # GPU order of the forward is unchanged: st depends on the fork point only.)
+            # The three LocalFuser calls run on that stream too, so their backward does (autograd
+            # replays a node on its forward's stream): on the main stream the fuser backward was
+            # enqueued behind the whole global backward and held the local backward there
+            # (29.58 / 29.61 vs 29.78 / 29.71 ms/step, gpurun r06g).  (Creating the local nodes
+            # after the global encoder's, so that autograd -- latest-created first -- enqueues the
+            # local backward as soon as its gradients exist, ran it beside the global backward
+            # but measured 29.75 / 29.80 vs 29.54 / 29.63: the chip is already busy, r06h.)
             main = torch.cuda.current_stream()
             st = tpgan_ops.side_streams(I128.device, 1, "local")[0] if tpgan_ops.MULTISTREAM else main
             st.wait_stream(main)
-            late = LOCAL_LATE["enabled"] and st is not main
-            if late:
-                enc = self.global_pathway.encode(I128, z)
             with torch.cuda.stream(st), tpgan_ops.concurrent(tpgan_ops.MULTISTREAM):
                 outs = LocalPathway.forward_group(paths, patches)
                 fused = self._fuse(outs, patches)
-            if not late:
-                enc = self.global_pathway.encode(I128, z)
+            enc = self.global_pathway.encode(I128, z)
             if st is not main:
                 main.wait_stream(st)
                 for t in [t for o in outs for t in o] + list(fused):
