@@ -259,6 +259,36 @@ int32_t tpg_l1_set_fwd(int32_t nseg, const tpg_l1_seg* segs, float* ws, size_t w
                        tpg_stream_t stream);
 int32_t tpg_l1_set_bwd(int32_t nseg, const tpg_l1_seg* segs, const float* gout, tpg_stream_t stream);
 
+/* SSD landmark head of the MobileNetV2 pretraining (MobileNetV2.py:342-649, batch 1 and per-point
+ * .item() loops in the reference; here one block per image).  All pointers are fp32 / int32 / u8
+ * device memory, dense:  pred (B, n, 2) pixel locations, cls (B, n, C) logits (C >= 5, class 4
+ * = background), truth (B, 8) four landmarks, keys (B, n) uniform [0, 1) draws.
+ *   tpg_ssd_loss_fwd  MultiTaskLoss.forward (:445-534): labels (B, n) = the landmark each anchor
+ *                     is assigned to (within the k (= int(ratio * n)) nearest of a landmark, the
+ *                     nearest such landmark, first on ties) or -1; sel (B, n) = 1 for the
+ *                     background anchors in the class loss (all of them, or the ones with the
+ *                     int(#positives * ratio_nb) smallest keys when there are more); terms
+ *                     (B, TPG_SSD_TERMS): [0] alpha * loc + beta * cls, [1..4] location MSE per
+ *                     landmark, [5..8] class CE per landmark, [9] background CE, [10] background
+ *                     count, [11..14] positives per landmark.  n <= TPG_SSD_MAXN, 1 <= k <= n.
+ *   tpg_ssd_loss_bwd  gradients of mean_b terms[b][0] times *gout (device scalar) w.r.t. pred
+ *                     (dloc) and cls (dcls), from the forward's labels / sel / terms.
+ *   tpg_ssd_decode    MultiTaskDecoder.forward (:551-597): per image and class, the anchors whose
+ *                     softmax confidence exceeds conf, greedy NMS (suppress within nms_thr,
+ *                     inclusive), the first top_k kept: keep (B, C, top_k) anchor indices (-1 =
+ *                     none), score (B, C, top_k). */
+#define TPG_SSD_TERMS 16
+#define TPG_SSD_MAXN 4096
+int32_t tpg_ssd_loss_fwd(int32_t B, int32_t n, int32_t C, const float* pred, const float* cls, const float* truth,
+                         float width, float height, int32_t k, double ratio_nb, float alpha, float beta,
+                         const float* keys, int32_t* labels, uint8_t* sel, float* terms, tpg_stream_t stream);
+int32_t tpg_ssd_loss_bwd(int32_t B, int32_t n, int32_t C, const float* pred, const float* cls, const float* truth,
+                         float width, float height, float alpha, float beta, const int32_t* labels,
+                         const uint8_t* sel, const float* terms, const float* gout, float* dloc, float* dcls,
+                         tpg_stream_t stream);
+int32_t tpg_ssd_decode(int32_t B, int32_t n, int32_t C, const float* loc, const float* cls, float conf, float nms_thr,
+                       int32_t top_k, int32_t* keep, float* score, tpg_stream_t stream);
+
 /* Depthwise Conv2d (groups == in_c == out_c, MobileNetV2.py:105), kernels up to 3x3, zero
  * padding: y = act(dwconv(x, w) + bias [+ res_scale * residual]).  w logical [C][1][kh][kw]
  * fp32 (any strides); x / y / residual channels-last, 16-byte aligned rows of desc.dtype. */

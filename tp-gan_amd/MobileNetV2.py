@@ -227,7 +227,12 @@ class MultiTaskLoss(nn.Module):
     the background samples (at most ratio_non_background x #positives, drawn uniformly
     without replacement when there are more) plus, per landmark, CE of its positives.  The
     reference takes batch 1; a batch here is the mean of the per-image losses.  `verbose`
-    prints the reference's per-term lines (:488, 516, 527)."""
+    prints the reference's per-term lines (:488, 516, 527).
+
+    Device tensors (fp32, <= 4096 anchors) run the HIP kernels (tpg_ssd_loss_fwd / _bwd: one
+    block per image does the assignment, the background draw from the same torch.rand keys as
+    the tensor form below, and the loss terms); CPU tensors -- the reference's own device in
+    Pretrain.py on a host without a GPU, and Temp.py -- keep the tensor form."""
 
     def __init__(self, alpha=None, beta=None, distance_threshold_ratio=0.1, ratio_non_background=None,
                  verbose=False):
@@ -240,9 +245,25 @@ class MultiTaskLoss(nn.Module):
                                      else ratio_non_background)
         self.verbose = verbose
 
+    def _hip(self, locations_pred):
+        # (float64 device tensors keep the tensor form: the kernels compute in fp32)
+        return locations_pred.is_cuda and locations_pred.shape[1] <= 4096 and locations_pred.dtype != torch.float64
+
     def get_positive_samples_and_classification_tensor(self, locations_pred, locations_true):
         """(positive index lists per landmark of image 0, labels (B, n) int: landmark or -1)."""
         B, n, _ = locations_pred.shape
+        if self._hip(locations_pred):
+            C = 5
+            cls0 = torch.zeros(B, n, C, device=locations_pred.device)
+            keys = torch.zeros(B, n, device=locations_pred.device)  # (no draw: only the labels are used)
+            with torch.no_grad():
+                k = int(self.distance_threshold_ratio * n)
+                if k < 1:
+                    raise ValueError("distance_threshold_ratio * anchors < 1: no positives can be chosen")
+                _, labels, _, _ = tpgan_ops._SsdLoss.apply(locations_pred.detach(), cls0, locations_true, keys, 1.0, 1.0,
+                                                           k, self.ratio_non_background, self.alpha, self.beta)
+            lists = [torch.nonzero(labels[0] == l).flatten().tolist() for l in range(4)]
+            return lists, labels
         true = locations_true.reshape(B, 4, 2).to(locations_pred.dtype)
         d = torch.cdist(locations_pred, true, p=2)                       # (B, n, 4)
         k = int(self.distance_threshold_ratio * n)
@@ -257,6 +278,23 @@ class MultiTaskLoss(nn.Module):
 
     def forward(self, locations_pred, classifications_pred, locations_true, image_size):
         B, n, _ = locations_pred.shape
+        if self._hip(locations_pred):
+            total, labels, sel, terms = tpgan_ops.ssd_loss(locations_pred, classifications_pred, locations_true,
+                                                           image_size, self.distance_threshold_ratio,
+                                                           self.ratio_non_background, self.alpha, self.beta)
+            if self.verbose:
+                t = terms[0].tolist()
+                for l in range(4):
+                    if t[11 + l] > 0:
+                        print("location loss %d               : %.4f * %s = %.4f" % (l, t[1 + l], self.alpha,
+                                                                                     t[1 + l] * self.alpha))
+                if t[10] > 0:
+                    print("background classification loss: %.4f * %s = %.4f" % (t[9], self.beta, t[9] * self.beta))
+                for l in range(4):
+                    if t[11 + l] > 0:
+                        print("classification loss %d         : %.4f * %s = %.4f" % (l, t[5 + l], self.beta,
+                                                                                     t[5 + l] * self.beta))
+            return total.to(locations_pred.dtype)
         _, labels = self.get_positive_samples_and_classification_tensor(locations_pred, locations_true)
         labels = labels.long()
         height, width = image_size
@@ -314,6 +352,23 @@ class MultiTaskDecoder(nn.Module):
         self.nms_distance_threshold = nms_distance_threshold
 
     def forward(self, locations, classifications):
+        if (locations.is_cuda and locations.shape[1] <= 4096 and classifications.shape[2] >= 5 and
+                locations.dtype != torch.float64):
+            # (tpg_ssd_decode: one block per image and class; the kept points in score order)
+            keep, score = tpgan_ops.ssd_decode(locations, classifications, self.confidence_threshold,
+                                               self.nms_distance_threshold, self.top_k)
+            keep, score = keep.cpu(), score.cpu()
+            output = []
+            for i in range(locations.shape[0]):
+                results = []
+                for c in range(classifications.shape[2]):
+                    for r in range(self.top_k):
+                        j = int(keep[i, c, r])
+                        if j < 0:
+                            break
+                        results.append((c, score[i, c, r].to(locations.device), locations[i, j]))
+                output.append(results)
+            return output
         scores = torch.softmax(classifications, dim=-1)
         output = []
         for i in range(locations.shape[0]):

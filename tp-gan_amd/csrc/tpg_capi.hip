@@ -1565,3 +1565,50 @@ extern "C" int32_t tpg_get_deterministic(void) { return tpg::deterministic(); }
 
 extern "C" const char* tpg_version(void) { return "tpgan_hip 0.1 gfx950"; }
 extern "C" const char* tpg_last_error(void) { return g_err.c_str(); }
+
+// ---- SSD landmark head (MobileNetV2.py:342-649; tpg_ssd.hip)
+static int32_t check_ssd(int32_t B, int32_t n, int32_t C, const void* pred, const void* cls, const char* who) {
+  if (B < 1 || n < 1 || n > TPG_SSD_MAXN || C < 5) return fail(-2, "%s: B %d, n %d (1..%d), C %d (>= 5)", who, B, n,
+                                                              TPG_SSD_MAXN, C);
+  if (!pred || !cls) return fail(-10, "%s: NULL input", who);
+  if (((uintptr_t)pred | (uintptr_t)cls) % 4) return fail(-15, "%s: inputs must be 4-byte aligned", who);
+  return 0;
+}
+
+extern "C" int32_t tpg_ssd_loss_fwd(int32_t B, int32_t n, int32_t C, const float* pred, const float* cls,
+                                    const float* truth, float width, float height, int32_t k, double ratio_nb,
+                                    float alpha, float beta, const float* keys, int32_t* labels, uint8_t* sel,
+                                    float* terms, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc = check_ssd(B, n, C, pred, cls, "ssd_loss_fwd");
+  if (rc) return rc;
+  if (!truth || !keys || !labels || !sel || !terms) return fail(-10, "ssd_loss_fwd: NULL buffer");
+  if (!(width > 0.f) || !(height > 0.f)) return fail(-2, "ssd_loss_fwd: image size must be positive");
+  if (k < 1 || k > n) return fail(-2, "ssd_loss_fwd: k = %d outside 1..%d", k, n);
+  return hip_check(launch_ssd_loss_fwd(B, n, C, k, pred, cls, truth, width, height, ratio_nb, alpha, beta, keys, labels,
+                                       sel, terms, (hipStream_t)stream), "ssd_loss_fwd");
+}
+
+extern "C" int32_t tpg_ssd_loss_bwd(int32_t B, int32_t n, int32_t C, const float* pred, const float* cls,
+                                    const float* truth, float width, float height, float alpha, float beta,
+                                    const int32_t* labels, const uint8_t* sel, const float* terms, const float* gout,
+                                    float* dloc, float* dcls, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc = check_ssd(B, n, C, pred, cls, "ssd_loss_bwd");
+  if (rc) return rc;
+  if (!truth || !labels || !sel || !terms || !gout || !dloc || !dcls) return fail(-10, "ssd_loss_bwd: NULL buffer");
+  if (!(width > 0.f) || !(height > 0.f)) return fail(-2, "ssd_loss_bwd: image size must be positive");
+  return hip_check(launch_ssd_loss_bwd(B, n, C, pred, cls, truth, width, height, alpha, beta, labels, sel, terms, gout,
+                                       dloc, dcls, (hipStream_t)stream), "ssd_loss_bwd");
+}
+
+extern "C" int32_t tpg_ssd_decode(int32_t B, int32_t n, int32_t C, const float* loc, const float* cls, float conf,
+                                  float nms_thr, int32_t top_k, int32_t* keep, float* score, tpg_stream_t stream) {
+  TPG_GROUP_SYNC();
+  int32_t rc = check_ssd(B, n, C, loc, cls, "ssd_decode");
+  if (rc) return rc;
+  if (top_k < 1 || top_k > 64) return fail(-2, "ssd_decode: top_k %d outside 1..64", top_k);
+  if (!keep || !score) return fail(-10, "ssd_decode: NULL output");
+  return hip_check(launch_ssd_decode(B, n, C, loc, cls, conf, nms_thr, top_k, keep, score, (hipStream_t)stream),
+                   "ssd_decode");
+}

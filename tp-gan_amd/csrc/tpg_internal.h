@@ -533,6 +533,15 @@ int launch_image_losses(int n, int c, int h, int w, const tpg_tensor& x, const t
                         float w_tv, float* part, const float* gout, float* out, const tpg_tensor* dx, hipStream_t st);
 int launch_l1_set(int nseg, const tpg_l1_seg* segs, float* part, const float* gout, float* out, bool bwd,
                   hipStream_t st);
+// SSD landmark head (tpg_ssd.hip): MultiTaskLoss assignment + loss, its backward, the decoder
+int launch_ssd_loss_fwd(int B, int n, int C, int k, const float* pred, const float* cls, const float* truth, float width,
+                        float height, double ratio_nb, float alpha, float beta, const float* keys, int* labels,
+                        unsigned char* sel, float* terms, hipStream_t s);
+int launch_ssd_loss_bwd(int B, int n, int C, const float* pred, const float* cls, const float* truth, float width,
+                        float height, float alpha, float beta, const int* labels, const unsigned char* sel,
+                        const float* terms, const float* gout, float* dloc, float* dcls, hipStream_t s);
+int launch_ssd_decode(int B, int n, int C, const float* loc, const float* cls, float conf, float nms_thr, int top_k,
+                      int* keep, float* score, hipStream_t s);
 int pw_tile_bm(int cfg);
 int pw_tile_bn(int cfg);
 int launch_pack_halo(const PackArgs& a, int nks, int bn, int ntiles, hipStream_t s);

@@ -19,6 +19,7 @@ if os.environ.get("TPG_LIB_PATH"):  # A/B builds of the same library (tools/ onl
 
 TPG_F32, TPG_BF16, TPG_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3
+SSD_TERMS, SSD_MAXN = 16, 4096  # (include/tpgan.h TPG_SSD_TERMS / TPG_SSD_MAXN)
 PAD_ZERO, PAD_REFLECT = 0, 1
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
 
@@ -118,6 +119,12 @@ EXPORTS = {
     "tpg_l1_set_fwd": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(L1Seg), ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "tpg_l1_set_bwd": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(L1Seg), ctypes.c_void_p, ctypes.c_void_p]),
+    "tpg_ssd_loss_fwd": (ctypes.c_int32, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_float] * 2 +
+                         [ctypes.c_int32, ctypes.c_double, ctypes.c_float, ctypes.c_float] + [ctypes.c_void_p] * 5),
+    "tpg_ssd_loss_bwd": (ctypes.c_int32, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_float] * 4 +
+                         [ctypes.c_void_p] * 7),
+    "tpg_ssd_decode": (ctypes.c_int32, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 2 + [ctypes.c_float] * 2 +
+                       [ctypes.c_int32] + [ctypes.c_void_p] * 3),
     "tpg_set_deterministic": (None, [ctypes.c_int32]),
     "tpg_group_begin": (None, []),
     "tpg_group_member": (None, []),

@@ -20,8 +20,8 @@ import torch
 
 from tpgan_lib import (ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU6, FLAG_CONCURRENT, FLAG_DX_ACCUM, FLAG_WPACKED, OP_BWD_DATA, OP_FWD,
                        PAD_REFLECT,
-                       PAD_ZERO, TPG_BF16, TPG_F32, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code, load,
-                       stream_ptr, tt)
+                       PAD_ZERO, SSD_TERMS, TPG_BF16, TPG_F32, ConvDesc, TpgTensor, check, dtype_code, dtype_from_code,
+                       load, stream_ptr, tt)
 
 _DTYPE = [torch.float32]
 
@@ -2102,3 +2102,64 @@ def linear_bn_act(x, lin, bn, act=None):
     else:
         y = batchnorm_train(conv2d(x4, w4, lin.bias), bn, act)
     return y.reshape(b, out_f)
+
+
+# ---- SSD landmark head of the MobileNetV2 pretraining (MobileNetV2.py:342-649; tpg_ssd.hip):
+# MultiTaskLoss / MultiTaskDecoder on device tensors.  The background draw's uniform keys are
+# torch.rand of the caller's generator state, the same draw as MobileNetV2.MultiTaskLoss's aten
+# form, so the two forms select the same background anchors.
+class _SsdLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, cls, truth, keys, width, height, k, ratio_nb, alpha, beta):
+        lib = load()
+        B, n, C = cls.shape
+        pred = pred.float().contiguous()
+        cls = cls.float().contiguous()
+        truth = truth.reshape(B, 8).float().contiguous()
+        keys = keys.float().contiguous()
+        labels = torch.empty(B, n, dtype=torch.int32, device=pred.device)
+        sel = torch.empty(B, n, dtype=torch.uint8, device=pred.device)
+        terms = torch.empty(B, SSD_TERMS, dtype=torch.float32, device=pred.device)
+        check(lib.tpg_ssd_loss_fwd(B, n, C, pred.data_ptr(), cls.data_ptr(), truth.data_ptr(), float(width),
+                                   float(height), int(k), float(ratio_nb), float(alpha), float(beta),
+                                   keys.data_ptr(), labels.data_ptr(), sel.data_ptr(), terms.data_ptr(), stream_ptr()))
+        ctx.save_for_backward(pred, cls, truth, labels, sel, terms)
+        ctx.cfg = (float(width), float(height), float(alpha), float(beta))
+        ctx.mark_non_differentiable(labels, sel, terms)
+        return terms[:, 0].mean(), labels, sel, terms
+
+    @staticmethod
+    def backward(ctx, g, _gl, _gs, _gt):
+        lib = load()
+        pred, cls, truth, labels, sel, terms = ctx.saved_tensors
+        B, n, C = cls.shape
+        width, height, alpha, beta = ctx.cfg
+        gout = g.reshape(1).float().contiguous()
+        dloc = torch.empty_like(pred)
+        dcls = torch.empty_like(cls)
+        check(lib.tpg_ssd_loss_bwd(B, n, C, pred.data_ptr(), cls.data_ptr(), truth.data_ptr(), width, height, alpha,
+                                   beta, labels.data_ptr(), sel.data_ptr(), terms.data_ptr(), gout.data_ptr(),
+                                   dloc.data_ptr(), dcls.data_ptr(), stream_ptr()))
+        return dloc, dcls, None, None, None, None, None, None, None, None
+
+
+def ssd_loss(pred, cls, truth, image_size, ratio, ratio_nb, alpha, beta):
+    """(mean over images of alpha * loc + beta * cls, labels (B, n) int32, background draw (B, n)
+    u8, per-image terms (B, 16): tpg_ssd_loss_fwd's layout)."""
+    height, width = image_size
+    keys = torch.rand(pred.shape[0], pred.shape[1], device=pred.device)
+    k = int(ratio * pred.shape[1])  # (MobileNetV2.py:393, in double precision as there)
+    return _SsdLoss.apply(pred, cls, truth, keys, width, height, k, ratio_nb, alpha, beta)
+
+
+def ssd_decode(loc, cls, conf, nms_thr, top_k):
+    """(keep (B, C, top_k) anchor indices or -1, score (B, C, top_k)) of tpg_ssd_decode."""
+    lib = load()
+    B, n, C = cls.shape
+    loc = loc.float().contiguous()
+    cls = cls.float().contiguous()
+    keep = torch.empty(B, C, top_k, dtype=torch.int32, device=loc.device)
+    score = torch.empty(B, C, top_k, dtype=torch.float32, device=loc.device)
+    check(lib.tpg_ssd_decode(B, n, C, loc.data_ptr(), cls.data_ptr(), float(conf), float(nms_thr), int(top_k),
+                             keep.data_ptr(), score.data_ptr(), stream_ptr()))
+    return keep, score
