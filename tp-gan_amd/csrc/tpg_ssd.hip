@@ -301,8 +301,11 @@ int launch_ssd_loss_fwd(int B, int n, int C, int k, const float* pred, const flo
                         unsigned char* sel, float* terms, hipStream_t s) {
   SsdArgs a{B, n, C, k, pred, cls, truth, width, height, ratio_nb, alpha, beta, keys, labels, sel, terms};
   const size_t lds = ssd_fwd_lds(n);
+  // (the largest dynamic size any n <= TPG_SSD_MAXN needs: the whole 160 KiB would leave no room
+  // for the kernel's static LDS, and the failed attribute call makes the launch report an error)
   static bool once = ((void)hipFuncSetAttribute((const void*)ssd_loss_fwd_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), true);
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)ssd_fwd_lds(TPG_SSD_MAXN)), true);
   (void)once;
   hipLaunchKernelGGL(ssd_loss_fwd_kernel, dim3(B), dim3(SSD_T), lds, s, a);
   return (int)hipGetLastError();
@@ -326,7 +329,7 @@ int launch_ssd_decode(int B, int n, int C, const float* loc, const float* cls, f
   while (n2 < n) n2 <<= 1;
   const size_t lds = (size_t)n2 * 12;
   static bool once = ((void)hipFuncSetAttribute((const void*)ssd_decode_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), true);
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, TPG_SSD_MAXN * 12), true);
   (void)once;
   hipLaunchKernelGGL(ssd_decode_kernel, dim3(B, C), dim3(SSD_T), lds, s, a);
   return (int)hipGetLastError();
