@@ -124,6 +124,9 @@ def timed(fn, iters, graph):
     return e0.elapsed_time(e1) / iters
 
 
+SWEEP = {"algos": tuple(range(1, 13)), "ks": (1, 2, 4, 8, 16, 32, 64)}  # (--wg-sweep candidates)
+
+
 def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=(), dalgo=0):
     lib = load()
     dev = torch.device("cuda", 0)
@@ -177,8 +180,8 @@ def run(name, s, iters, passes, sweep=False, wg_algo=0, graph=False, dsplits=(),
     f = flops(s)
     if sweep:  # every weight-gradient (algo, pixel split) the tuner would try
         res = []
-        for algo in range(1, 13):
-            for ks in (1, 2, 4, 8, 16, 32, 64):
+        for algo in SWEEP["algos"]:
+            for ks in SWEEP["ks"]:
                 d.algo, d.ksplit = algo, ks
                 rc = lib.tpg_conv2d_bwd_filter(ctypes.byref(d), tt(x), tt(g), tt(dw), None, 0, stream_ptr())
                 if rc:
@@ -228,6 +231,8 @@ def main():
     ap.add_argument("--wg-sweep", action="store_true", help="time every weight-gradient algo / pixel split")
     ap.add_argument("--wg-algo", default="",
                     help="weight-gradient algo[/pixel splits] per shape, e.g. enhance_128=12/1,add_128=7")
+    ap.add_argument("--sweep-algos", default="", help="--wg-sweep: these algos only, e.g. 7,12")
+    ap.add_argument("--sweep-ks", default="", help="--wg-sweep: these pixel splits, e.g. 16,24,29,32")
     ap.add_argument("--graph", action="store_true", help="time graph replays (GPU time of short kernels)")
     ap.add_argument("--r50", action="store_true", help="the ResNet-50 identity extractor's shapes (configs[2])")
     ap.add_argument("--dsplits", default="", help="also time forced fwd / dgrad k splits, e.g. 1,2,4,8")
@@ -235,6 +240,10 @@ def main():
     ap.add_argument("--tune-file", default=None,
                     help="weight-gradient picks saved by a train step (bench.py with TPG_TUNE_DUMP=path)")
     a = ap.parse_args()
+    if a.sweep_algos:
+        SWEEP["algos"] = tuple(int(v) for v in a.sweep_algos.split(","))
+    if a.sweep_ks:
+        SWEEP["ks"] = tuple(int(v) for v in a.sweep_ks.split(","))
     if a.tune_file:
         T.load_tuning(a.tune_file)
     shapes = {k: v[0] for k, v in R50.items()} if a.r50 else SHAPES
