@@ -420,14 +420,10 @@ def test_prepacked_weights_match_inline_packing(gpu):
     tr.step(b)  # (the first step also re-lays the flat buffers out in gradient-completion order)
     tr.step(b)
     torch.cuda.synchronize()
-    # images re-packed after the update: one batched table for the whole network, one per op
-    # (the forward images after Adam, the input-gradient ones at the next step's start:
-    # tpgan_train.DEFER_BWD_IMAGES), or per bucket when G's Adam ran bucket by bucket under the
-    # backward (TPGANTrainer.overlap_optimizer)
+    # images re-packed after the update: one batched table for the whole network, or per bucket
+    # when G's Adam ran bucket by bucket under the backward (TPGANTrainer.overlap_optimizer)
     assert len(tr.fG.pack_entries) > 50
-    op_packs = getattr(tr.fG, "op_packs", None)
-    assert (tr.fG.pack_table is not None or (op_packs is not None and len(op_packs[1]) == 2) or
-            (tr.overlap_optimizer and tr.fG.range_packs[1]))
+    assert tr.fG.pack_table is not None or (tr.overlap_optimizer and tr.fG.range_packs[1])
 
     def run():
         x = b["I128"].clone().requires_grad_(True)

@@ -245,7 +245,6 @@ struct WgradRHArgs {
                               // A fragment; k-tile kt is summed by tile (kt % bshare) of the a-tile's
                               // (b, row, tap) tiles (bshare = 1: the first one, deterministic)
   int bshare;
-  int late;                   // next k-tile's DMAs behind the first fragment reads (LATE variant)
 };
 
 // ---------------------------------------------------------------- weight packing ----

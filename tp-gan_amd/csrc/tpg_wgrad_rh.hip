@@ -61,19 +61,8 @@ __device__ __forceinline__ int rh_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-// The tiles whose kernel fits 128 VGPRs (two 512-thread blocks per CU); the LATE variant is
-// built for them only, held to the same budget.
-template <int NR, int NT, int BM, int BC>
-constexpr bool rh_fits128() {
-  return NR == 2 || (NR == 1 && ((BM == 128 && BC == 32 && NT <= 5) || (BM == 64 && BC == 64 && NT <= 4) ||
-                                 (BM == 64 && BC == 32)));
-}
-
-// LATE: the DMAs of k-tile kt+2 are issued inside k-tile kt's compute, behind its first
-// substep's fragment reads (as the halo kernel's next-step weight DMA), instead of ahead of them:
-// the fragment reads no longer queue behind 24 KB of LDS-DMA writes
-template <int DT, int NR, int NT, int BM, int BC, bool LATE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LATE ? 4 : 1))) void wgrad_rh_kernel(const WgradRHArgs p) {
+template <int DT, int NR, int NT, int BM, int BC>
+__global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   // k-tile: 64 pixels = TH x TW (TW = p.tw: a row segment of 64, or TH = 64 / TW whole rows of
   // a narrower map); block taps: NR kernel rows x NT columns (row mode NR = 1, image mode
   // NR = kh), all read from one (TH + NR - 1) x (TW + NT - 1) X halo of the k-tile
@@ -239,7 +228,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LATE ? 4 : 
     }
   // BIAS (compile-time): the bias MFMAs sit beside the regular MFMA holding each A fragment
   // (see tpg_wgrad2.hip: no runtime branch inside this hand-scheduled region)
-  auto compute = [&](int slot, bool bias_now, auto&& dma) {
+  auto compute = [&](int slot, bool bias_now) {
     const char* A = lds + slot * STAGE;
     const char* B = A + BYTES_A;
     constexpr int NS = KP / 32;
@@ -276,10 +265,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LATE ? 4 : 
       else h[0][rr] = s16x4{(short)lane, 1, 2, 3};
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (LATE) {
-      dma();
-      __builtin_amdgcn_sched_barrier(0);
-    }
 #pragma unroll
     for (int ks = 0; ks < NS; ++ks) {
       const int cur = ks & 1;
@@ -355,9 +340,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LATE ? 4 : 
   RH_WAIT_BARRIER();  // retires k-tile 0
   int slot = 0;
   for (int kt = 0; kt < nkt; ++kt) {
-    const int nslot = slot == 0 ? 2 : slot - 1;
-    if constexpr (!LATE) issue_next(nslot);
-    compute(slot, bias_wave && (kt0 + kt) % p.bshare == sid, [&] { issue_next(nslot); });  // (one inlined copy)
+    issue_next(slot == 0 ? 2 : slot - 1);
+    compute(slot, bias_wave && (kt0 + kt) % p.bshare == sid);  // (one inlined copy)
     RH_WAIT_BARRIER();  // retires k-tile kt+1, kt+2 stays in flight
     slot = slot == 2 ? 0 : slot + 1;
   }
@@ -466,19 +450,13 @@ template <int NR, int NT, int BM, int BC>
 static int launch_rh_t(const WgradRHArgs& a, hipStream_t s) {
   constexpr int GB = (((NR == 1 ? 72 : 200) * BC * 2 + 1023) / 1024 + 7) / 8;
   const size_t lds = 3 * (64 * BM * 2 + GB * 8 * 1024);
-  constexpr bool CL = rh_fits128<NR, NT, BM, BC>();
-  auto k1 = wgrad_rh_kernel<1, NR, NT, BM, BC, false>;
-  auto k2 = wgrad_rh_kernel<2, NR, NT, BM, BC, false>;
-  auto l1 = wgrad_rh_kernel<1, NR, NT, BM, BC, CL>;
-  auto l2 = wgrad_rh_kernel<2, NR, NT, BM, BC, CL>;
+  auto k1 = wgrad_rh_kernel<1, NR, NT, BM, BC>;
+  auto k2 = wgrad_rh_kernel<2, NR, NT, BM, BC>;
   static bool once = ((void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                       (void)hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                      (void)hipFuncSetAttribute((const void*)l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                      (void)hipFuncSetAttribute((const void*)l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                       true);
   (void)once;
-  hipLaunchKernelGGL(a.late ? (a.dtype == 2 ? l2 : l1) : (a.dtype == 2 ? k2 : k1), dim3(a.tiles * a.ksplit), dim3(512),
-                     lds, s, a);
+  hipLaunchKernelGGL(a.dtype == 2 ? k2 : k1, dim3(a.tiles * a.ksplit), dim3(512), lds, s, a);
   return (int)hipGetLastError();
 }
 
