@@ -332,34 +332,6 @@ def test_identity_side_stream_bit_identical(gpu):
     assert res[True][2] == res[False][2]
 
 
-def test_deferred_bwd_images_bit_identical(gpu):
-    """tpgan_train.DEFER_BWD_IMAGES: G's input-gradient weight images re-packed on a side stream
-    at the start of the next step (under G's forward) instead of in phase C give the same
-    steps, bit for bit (deterministic bf16); with it on, phase C really leaves them stale."""
-    import tpgan_ops
-    import tpgan_train
-    prev = tpgan_train.DEFER_BWD_IMAGES["enabled"]
-    res = {}
-    try:
-        with tpgan_ops.deterministic():
-            for on in (False, True):
-                tpgan_train.DEFER_BWD_IMAGES["enabled"] = on
-                G, D = _models(gpu)
-                tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16,
-                                              use_dropout=False)
-                b = tpgan_train.synthetic_batch(2, gpu, seed=23)
-                outs = [tr.step(b) for _ in range(3)]
-                torch.cuda.synchronize()
-                stale = [e for k, e in tr.fG.pack_entries.items()
-                         if e is not None and e.njobs and k[0] == tpgan_ops.OP_BWD_DATA and e.epoch != tr.fG.epoch]
-                res[on] = (tr.fG.data.clone(), tr.fD.data.clone(), [float(o["loss_G"]) for o in outs], len(stale))
-    finally:
-        tpgan_train.DEFER_BWD_IMAGES["enabled"] = prev
-    assert res[False][3] == 0 and res[True][3] > 10, (res[False][3], res[True][3])
-    assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
-    assert res[True][2] == res[False][2]
-
-
 def test_gradient_penalty_double_backward_vs_oracle(gpu):
     """WGAN-GP through the HIP double backward: the penalty and D's parameter gradients
     of it against torch's double backward of the oracle D (float64 CPU), global 1e-3."""

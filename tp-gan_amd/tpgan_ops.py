@@ -561,35 +561,19 @@ def _packed_weight(param, d, op, w):
     return e.buf
 
 
-def _pack_table(lib, entries, device):
-    raw = b"".join(e.jobs for e in entries)
-    n = sum(e.njobs for e in entries)
-    host = ctypes.create_string_buffer(raw, len(raw))
-    nblocks = lib.tpg_pack_prepare(host, n)
-    return (torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(device), n, nblocks)
-
-
-def repack(flat, ops=None):
-    """Re-pack the weight images of `flat` in one launch (after its parameters changed): every
-    image, or those of the given ops only (OP_FWD / OP_BWD_DATA; the tables of such subsets are
-    cached per pack_version, as repack_range's)."""
-    entries = [e for k, e in flat.pack_entries.items() if e is not None and e.njobs and (ops is None or k[0] in ops)]
+def repack(flat):
+    """Re-pack every weight image of `flat` in one launch (after its parameters changed)."""
+    entries = [e for e in flat.pack_entries.values() if e is not None and e.njobs]
     if not entries:
         return
     lib = load()
-    if ops is None:
-        if flat.pack_table is None:
-            flat.pack_table = _pack_table(lib, entries, flat.data.device)
-        dev, n, nblocks = flat.pack_table
-    else:
-        ver = getattr(flat, "pack_version", 0)
-        cache = getattr(flat, "op_packs", None)
-        if cache is None or cache[0] != ver:
-            cache = flat.op_packs = (ver, {})
-        key = tuple(sorted(ops))
-        if key not in cache[1]:
-            cache[1][key] = _pack_table(lib, entries, flat.data.device)
-        dev, n, nblocks = cache[1][key]
+    if flat.pack_table is None:
+        raw = b"".join(e.jobs for e in entries)
+        n = sum(e.njobs for e in entries)
+        host = ctypes.create_string_buffer(raw, len(raw))
+        nblocks = lib.tpg_pack_prepare(host, n)
+        flat.pack_table = (torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(flat.data.device), n, nblocks)
+    dev, n, nblocks = flat.pack_table
     check(lib.tpg_pack_run(dev.data_ptr(), n, nblocks, stream_ptr()))
     for e in entries:
         e.epoch = flat.epoch

@@ -103,13 +103,10 @@ class FlatParams:
     def zero_grad(self):
         self.grad.zero_()
 
-    def adam(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0, check_finite=False,
-             defer_bwd_images=False):
+    def adam(self, lr, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0, check_finite=False):
         """One Adam update of the whole network (one launch).  check_finite (the loss-scaled
         fp16 step): an inf / NaN anywhere in the gradients skips the update on the device --
-        parameters, moments and the step counter stay as they were (last_step_skipped()).
-        defer_bwd_images: re-pack only the forward weight images here; the caller re-packs the
-        input-gradient images (repack_bwd_images) before the next backward."""
+        parameters, moments and the step counter stay as they were (last_step_skipped())."""
         self.step += 1
         if check_finite:
             tpgan_ops.grad_check(self.grad, self.adam_state)
@@ -122,12 +119,7 @@ class FlatParams:
         if check_finite:  # (on the device: no synchronisation; skipped_steps() reads it)
             self.skipped.add_(self.adam_state[3].ne(0).float())
         self.epoch += 1
-        tpgan_ops.repack(self, ops=(tpgan_ops.OP_FWD,) if defer_bwd_images else None)
-
-    def repack_bwd_images(self):
-        """The input-gradient weight images at the current parameters (after adam(...,
-        defer_bwd_images=True))."""
-        tpgan_ops.repack(self, ops=(tpgan_ops.OP_BWD_DATA,))
+        tpgan_ops.repack(self)
 
     def skipped_steps(self):
         """Updates skipped for non-finite gradients so far (synchronises).  A run whose static
@@ -468,15 +460,9 @@ FUSED_LOSSES = {"enabled": True}
 # most of the chip idle: configs[2] eager 38.19 / 37.95 -> 34.50 / 35.41 ms/step (gpurun r05ak).
 # The stream is the real-image features' one (they ran in phase A): a process holding one more
 # stream crashed in the first replay of a later whole-step capture (r05aj-r05al; reusing the
-# stream, r05aq, it does not).  Inside capture() ("in_capture") since round 6: the round-5
-# hipStreamEndCapture crashes (r05ar) came from an event wait of that stream on itself, which
-# FeatureExtract no longer issues.  False: everything on the step's stream.
+# stream, r05aq, it does not).  Not inside capture() ("in_capture"): hipStreamEndCapture
+# crashed with the fork in the graph (r05ar).  False: everything on the step's stream.
 IDENTITY_STREAM = {"enabled": True, "in_capture": True, "own_stream": False}
-
-# G's Adam (phase C) re-packs only G's forward weight images; the input-gradient images are
-# re-packed on a side stream at the start of the next step, under G's forward, and joined
-# before G's backward (the only reader of them).  False: phase C re-packs every image (A/B).
-DEFER_BWD_IMAGES = {"enabled": True}
 
 
 def total_variation(x):
@@ -554,7 +540,6 @@ class TPGANTrainer:
         self.comm_events = []
         self.identity_fn = identity_fn
         self.identity_forks_captured = 0  # identity side-stream forks recorded inside capture()
-        self._bwd_pack = None  # the side stream re-packing G's input-gradient images (DEFER_BWD_IMAGES)
         self.sync.broadcast(self.fG)
         self.sync.broadcast(self.fD)
 
@@ -615,17 +600,6 @@ class TPGANTrainer:
     def _phase_a(self, b):
         G, D = self.G, self.D
         self.fG.zero_grad()
-        self._bwd_pack = None
-        if self._defer_bwd_images():
-            # G's input-gradient images at the weights phase C left (DEFER_BWD_IMAGES)
-            main = torch.cuda.current_stream()
-            st = tpgan_ops.side_streams(self.fG.data.device, 1, "repack")[0]
-            st.wait_stream(main)
-            with torch.cuda.stream(st):
-                self.fG.repack_bwd_images()
-            self._bwd_pack = st
-            if self._capturing and self._segmented:  # (each phase is a graph of its own: join now)
-                self._join_bwd_pack()
         # D(real) of this batch already ran at the end of the previous step (_real_ahead): its
         # gradient is in fD.grad and its output is kept for the loss
         d_real_pre, self._d_real_next = self._d_real_next, None
@@ -666,15 +640,6 @@ class TPGANTrainer:
                 with tpgan_ops.wgrad_side_stream():  # (weight gradients overlap the next input gradients)
                     (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
-
-    def _defer_bwd_images(self):
-        return (DEFER_BWD_IMAGES["enabled"] and self.fG.data.is_cuda and tpgan_ops.MULTISTREAM and
-                not (self.gsync is not None and self.gsync.optimizer is not None))
-
-    def _join_bwd_pack(self):
-        if self._bwd_pack is not None:
-            torch.cuda.current_stream().wait_stream(self._bwd_pack)
-            self._bwd_pack = None
 
     def _real_ahead(self, nb):
         """The next step's D(real) forward and backward of -mean D(real) into a fresh fD.grad
@@ -777,7 +742,6 @@ class TPGANTrainer:
             if self.gsync.optimizer is not None:
                 self.fG.adam_begin(self.betas)  # (the step counter, once, ahead of every bucket's update)
             self.gsync.begin()
-        self._join_bwd_pack()
         with tpgan_ops.roctx_range("G-bwd"), tpgan_ops.wgrad_side_stream():
             (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
         self._st["loss_G"] = loss_G.detach()
@@ -821,7 +785,7 @@ class TPGANTrainer:
                 self.fG.adam_end()
             else:
                 self.fG.adam(self.lr, self.betas, grad_scale=self.sync.grad_scale / self.loss_scale,
-                             check_finite=self.loss_scale != 1.0, defer_bwd_images=self._defer_bwd_images())
+                             check_finite=self.loss_scale != 1.0)
         out = {"loss_D": self._st["loss_D"], "loss_G": self._st["loss_G"]}
         if self.loss_scale != 1.0:  # device tensors: reading them is the caller's synchronisation
             out["skipped_D"], out["skipped_G"] = self.fD.skipped, self.fG.skipped
@@ -978,9 +942,6 @@ class TPGANTrainer:
         # steps updated G bucket by bucket and never needed it); the images are re-packed unchanged
         tpgan_ops.repack(self.fG)
         tpgan_ops.repack(self.fD)
-        if self._defer_bwd_images():  # (and the two halves' tables of G, DEFER_BWD_IMAGES)
-            tpgan_ops.repack(self.fG, ops=(tpgan_ops.OP_FWD,))
-            tpgan_ops.repack(self.fG, ops=(tpgan_ops.OP_BWD_DATA,))
         torch.cuda.synchronize()
         self._capturing = True  # graph replays reduce G in one call between phases
         self._segmented = bool(segmented)
