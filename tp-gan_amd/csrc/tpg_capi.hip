@@ -61,6 +61,12 @@ static const int g_halo_pair = [] {
   const char* e = getenv("TPG_HALO_PAIR");
   return (e && e[0] == '0') ? 0 : 1;
 }();
+// wgrad_rh: MFMAs of all-padding blocks of edge tiles skipped (WgradRHArgs.skip); TPG_RH_SKIP=0
+// (read once at load) runs them, for same-box A/B runs
+static const int g_rh_skip = [] {
+  const char* e = getenv("TPG_RH_SKIP");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
 // kernel of the small-map multi-tap forward / input-gradient plans (desc.data_algo; 0 = rule)
 static thread_local int g_data_algo = 0;
 struct ShareScope {
@@ -1180,6 +1186,7 @@ static int32_t wgrad_rh(const tpg_conv_desc* d, const tpg_tensor& x, const tpg_t
   // bias MFMAs spread over up to 16 / ksplit tiles: same-address atomics serialise (~50 ns
   // each), so blocks x splits adding into one dbias row must stay few
   a.bshare = deterministic() ? 1 : std::max(1, std::min(a.ntb * a.nrg * cdiv(a.kw, a.nt), 16 / a.ksplit));
+  a.skip = g_rh_skip;
   TPG_GROUP_SYNC();
   return hip_check(launch_wgrad_rh(a, stream), "wgrad_rh");
 }

@@ -245,6 +245,7 @@ struct WgradRHArgs {
                               // A fragment; k-tile kt is summed by tile (kt % bshare) of the a-tile's
                               // (b, row, tap) tiles (bshare = 1: the first one, deterministic)
   int bshare;
+  int skip;                   // skip the MFMAs of all-padding 16 x 16 blocks of edge tiles
 };
 
 // ---------------------------------------------------------------- weight packing ----

@@ -61,8 +61,16 @@ __device__ __forceinline__ int rh_refl(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
+// The tiles held to 128 VGPRs (two 512-thread blocks per CU)
+template <int NR, int NT, int BM, int BC>
+constexpr bool rh_fits128() {
+  return NR == 2 || (NR == 1 && ((BM == 128 && BC == 32 && NT <= 5) || (BM == 64 && BC == 64 && NT <= 4) ||
+                                 (BM == 64 && BC == 32)));
+}
+
 template <int DT, int NR, int NT, int BM, int BC>
-__global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(rh_fits128<NR, NT, BM, BC>() ? 4 : 1)))
+void wgrad_rh_kernel(const WgradRHArgs p) {
   // k-tile: 64 pixels = TH x TW (TW = p.tw: a row segment of 64, or TH = 64 / TW whole rows of
   // a narrower map); block taps: NR kernel rows x NT columns (row mode NR = 1, image mode
   // NR = kh), all read from one (TH + NR - 1) x (TW + NT - 1) X halo of the k-tile
@@ -171,6 +179,25 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
   };
 
   const int wm = wave / WN, wn = wave % WN;
+  // MFMA blocks of a padded edge tile that hold no real dW element -- 16 rows at or past Ca, or
+  // 16 columns whose b channel is at or past Cb or whose tap is past the kernel -- read zeros;
+  // their MFMAs are skipped (p.skip; wave-uniform masks, a scalar branch per MFMA).  206
+  // channels pad to 256 rows x 224 columns per tap, a quarter of the MFMAs dead.
+  unsigned mlive = ~0u, jlive = ~0u;
+  if (p.skip) {
+    mlive = 0;
+    jlive = 0;
+#pragma unroll
+    for (int m = 0; m < MREP; ++m)
+      if (a0 + wm * WTM + m * 16 < p.Ca) mlive |= 1u << m;
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const int col = wn * WTN + j * 16, tap = col / BC;
+      if (b0 + col % BC < p.Cb && r0 + tap / NT < p.kh && s0 + tap % NT < p.kw) jlive |= 1u << j;
+    }
+    mlive = __builtin_amdgcn_readfirstlane(mlive);
+    jlive = __builtin_amdgcn_readfirstlane(jlive);
+  }
   const int g = lane >> 4, l16 = lane & 15;
   const int q = l16 >> 2, p4 = l16 & 3;
   const bool bias_wave = has_bias && wn == 0;
@@ -280,7 +307,9 @@ __global__ __launch_bounds__(512) void wgrad_rh_kernel(const WgradRHArgs p) {
         const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h[cur][2 * MREP + 2 * j],
                                                                              h[cur][2 * MREP + 2 * j + 1],
                                                                              0, 1, 2, 3, 4, 5, 6, 7));
-        if constexpr ((TPG_RH_ABL & 4) == 0) acc[m][j] = mfma16x16x32<DT>(av, bv, acc[m][j]);
+        if constexpr ((TPG_RH_ABL & 4) == 0) {
+          if ((mlive >> m) & (jlive >> j) & 1u) acc[m][j] = mfma16x16x32<DT>(av, bv, acc[m][j]);
+        }
         else acc[m][j][0] += (float)av[0] * (float)bv[1];
         if (ks + 1 < NS) {
 #pragma unroll
