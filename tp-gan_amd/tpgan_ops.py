@@ -282,6 +282,11 @@ AUTOTUNE = {"enabled": True, "cache": {}, "trials": 0, "frozen": False}
 # (adding the library's own split for each tile, which fills whole rounds of the chip and won
 # several isolated trials, measured 36.22-36.26 vs 36.10-36.14 ms/step in round 3)
 _WG_SPLITS = (1, 2, 4, 8, 16, 32, 64)
+# between the powers of two above 16 (whole-chip shapes only): the 128 x 32 row-halo tile of
+# enhance_128 (70 tiles) fills the chip's 512 resident blocks best at 36 splits -- 1.381 vs
+# 1.405 ms at 32 (tools/bench_layers.py --wg-sweep, gpurun r06n).  False: powers of two (A/B)
+WG_SPLITS_EXTRA = {"enabled": True}
+_WG_SPLITS_X = (1, 2, 4, 8, 16, 24, 32, 36, 48, 64)
 
 
 def _desc_tuple(d):
@@ -483,7 +488,7 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     best, best_ms = (0, 0), None
     torch.cuda.synchronize()
     for algo in range(1, 13):
-        for ks in _WG_SPLITS:
+        for ks in (_WG_SPLITS_X if WG_SPLITS_EXTRA["enabled"] else _WG_SPLITS):
             if ks > nkt or (ks > 16 and (d.flags & FLAG_CONCURRENT)):
                 break
             d.algo, d.ksplit = algo, ks
