@@ -525,38 +525,6 @@ def test_bucketed_optimizer_bit_identical(gpu):
         assert torch.equal(a, c)
 
 
-def test_wgrad_side_stream_bit_identical(gpu):
-    """Weight gradients on the side stream (tpgan_ops.wgrad_side_stream, TPG_WGRAD_SIDE=1)
-    against all of them on the launching stream: deterministic mode, bf16, from the
-    same state -- parameters, gradients and Adam moments bit-identical (a side-stream read of
-    a buffer the main stream already overwrote, or a missing join, would show here)."""
-    import tpgan_ops
-    import tpgan_train
-    G, D = _models(gpu)
-    tr = tpgan_train.TPGANTrainer(G, D, lr=LR, betas=BETAS, compute_dtype=torch.bfloat16, use_dropout=False)
-    b = tpgan_train.synthetic_batch(4, gpu, seed=19)
-    res = {}
-    with tpgan_ops.deterministic():
-        tr.step(b)
-        torch.cuda.synchronize()
-        snap = _snapshot(tr)
-        for on in (True, False, True):
-            tpgan_ops.WGRAD_SIDE["enabled"] = on
-            try:
-                _restore(tr, snap)
-                tr.step(b)
-                tr.step(b)
-                torch.cuda.synchronize()
-            finally:
-                tpgan_ops.WGRAD_SIDE["enabled"] = False
-            res.setdefault(on, []).append(
-                [t.clone() for t in (tr.fG.data, tr.fD.data, tr.fG.grad, tr.fD.grad, tr.fG.exp_avg_sq)])
-    for a, c in zip(res[True][0], res[False][0]):
-        assert torch.equal(a, c)
-    for a, c in zip(res[True][0], res[True][1]):
-        assert torch.equal(a, c)
-
-
 def test_bs32_step_properties(gpu):
     """The benchmark's configuration (bf16, bs32, flat params, autotuned kernels) against the
     same step in fp32 (deterministic) from the same weights and batch: losses finite and within

@@ -4,7 +4,7 @@ process, one trainer, variants alternated round by round: cdna_hip_programming.m
     python tools/ab_step.py [--steps 10] [--rounds 5] VARIANT [VARIANT ...]
 
 VARIANT = name[:module.ATTR[.key]=value,...], e.g.
-    base   side:tpgan_ops.WGRAD_SIDE.enabled=1   nogroup:tpgan_ops.GROUP.enabled=0   nt:env.TPG_OPT_VAR=3
+    base   nolink:tpgan_ops.ACT_LINK.enabled=0   nogroup:tpgan_ops.GROUP.enabled=0
 Values are parsed as int / float / bool literals.  Prints per-variant median and min ms/step.
 """
 import argparse

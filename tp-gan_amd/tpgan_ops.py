@@ -114,31 +114,6 @@ def concurrent(on=True):
         _CONCURRENT.pop()
 _SIDE = {}
 
-# Weight gradients on a side stream (wgrad_side_stream()): inside the block, a fused conv
-# backward launches its input gradient (and g) on the current stream and its weight / bias
-# gradient on a per-device side stream behind an event, so the next layer's input gradient
-# overlaps this layer's weight gradient; leaving the block joins the side stream.
-# (off by default: measured 37.86 / 37.97 ms/step with it vs 37.80 without -- the overlap
-# it buys is paid back in host time per layer (event, wait, record_stream), and the host
-# already spends ~31.6 ms enqueueing a ~38 ms step; WGRAD_SIDE["enabled"] = True turns it on)
-WGRAD_SIDE = {"stream": None, "enabled": False}
-
-
-@contextlib.contextmanager
-def wgrad_side_stream(device=None, on=True):
-    if not (on and WGRAD_SIDE["enabled"] and torch.cuda.is_available()):
-        yield
-        return
-    st = side_streams(device if device is not None else torch.cuda.current_device(), 1, "wgrad")[0]
-    prev = WGRAD_SIDE["stream"]
-    WGRAD_SIDE["stream"] = st
-    try:
-        yield
-    finally:
-        WGRAD_SIDE["stream"] = prev
-        torch.cuda.current_stream().wait_stream(st)
-
-
 def side_streams(device, n, tag=""):
     """n persistent side HIP streams of `device` (created once per (n, tag): users that may
     be in flight at the same time ask with different tags)."""
@@ -885,26 +860,16 @@ def _conv_act_backward_fused_body(ctx, gy, keep, lib, x, weight, y, d, dtype, n,
     fx = _fix_c1(dx) if dx is not None else None
     dwt = dwv if (need_dw and not tune_first) else None
     bptr = dbias.data_ptr() if dbias is not None else None
-    # weight / bias gradient on the side stream (only into the flat buffers: nothing autograd
-    # would accumulate on this stream); not while capturing a graph or probing
-    side = WGRAD_SIDE["stream"]
-    # (a residual block's last conv parks its g for the first conv's in-place dgrad, GradLink:
-    # its weight gradient stays on this stream, ahead of that write; a ConvTranspose2d sums its
-    # bias in the activation-backward pass, so it stays unsplit too)
-    split = (side is not None and not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
-             ctx.link_res is None and not ctx.geom.transposed and PROBE["match"] is None and
-             not torch.cuda.is_current_stream_capturing())
     # probing the weight gradient (bench.py roofline, tools/trace_step.py): the same two calls
     # as the side-stream split, both on this stream, events around the second -- the kernels
     # and their order on the stream are the fused call's (input gradient, then weight gradient)
     # (only where dW and the bias go into the flat buffers: a local dw buffer would otherwise be
     # dropped below.  A parked residual gradient is fine here: both calls stay on this stream,
     # ahead of the first conv's in-place write of it)
-    probe_w = (not split and not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
+    probe_w = (not grouped and dwt is not None and dw is None and (dbias is None or fused_b) and
                not ctx.geom.transposed and PROBE["match"] is not None and PROBE["match"](d, "wgrad") and
                not torch.cuda.is_current_stream_capturing())
-    if probe_w:
-        split = True
+    split = probe_w
     e0 = _probe_begin(d, "bwd")
     _run_maybe_packed(
         lambda: lib.tpg_conv2d_bwd(ctypes.byref(d), tt(x), _packed_tt(pk), tt(y), tt(gy), tt(g), tt(fx),
@@ -919,28 +884,15 @@ def _conv_act_backward_fused_body(ctx, gy, keep, lib, x, weight, y, d, dtype, n,
         gt = gy if g_is_gy else g  # (g now holds act'(y) * gy: the second call takes it as is)
         d2 = _plain_desc(d)
         d2.algo, d2.ksplit = d.algo, d.ksplit
-        if probe_w:
-            ew = _probe_begin(d, "wgrad")
-            check(lib.tpg_conv2d_bwd(ctypes.byref(d2), tt(x), tt(None), tt(None), tt(gt), tt(gt), tt(None), tt(dwt),
-                                     bptr, None, 0, stream_ptr()))
-            _probe_end(ew, d, "wgrad")
-            if fused_b:
-                _grad_ready(ctx.bparam)
-            _grad_ready(ctx.wparam)
-        else:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                check(lib.tpg_conv2d_bwd(ctypes.byref(d2), tt(x), tt(None), tt(None), tt(gt), tt(gt), tt(None),
-                                         tt(dwt), bptr, None, 0, stream_ptr()))
-                if fused_b:
-                    _grad_ready(ctx.bparam)
-                _grad_ready(ctx.wparam)
-            for t in (x, gt):  # (their memory stays reserved until the side stream has read it)
-                t.record_stream(side)
+        ew = _probe_begin(d, "wgrad")
+        check(lib.tpg_conv2d_bwd(ctypes.byref(d2), tt(x), tt(None), tt(None), tt(gt), tt(gt), tt(None), tt(dwt),
+                                 bptr, None, 0, stream_ptr()))
+        _probe_end(ew, d, "wgrad")
+        if fused_b:
+            _grad_ready(ctx.bparam)
+        _grad_ready(ctx.wparam)
         fused_b = False
-        dbias = None  # (accumulated into the flat buffer on the side stream)
+        dbias = None  # (accumulated into the flat buffer by the second call)
         dw = None
         need_dw = False
     if acc is not None and dx is not None:  # (not accumulated in the launch: shape / dtype mismatch)

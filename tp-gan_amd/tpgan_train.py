@@ -637,8 +637,7 @@ class TPGANTrainer:
                     loss_D = loss_D + self.w["weight_gradient_penalty"] * self.gradient_penalty(real, fake.detach())
                 if self.dsync is not None and not self._capturing:
                     self.dsync.begin()
-                with tpgan_ops.wgrad_side_stream():  # (weight gradients overlap the next input gradients)
-                    (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
+                (loss_D * self.loss_scale if self.loss_scale != 1.0 else loss_D).backward()
         self._st = {"outs": outs, "loss_D": loss_D.detach()}
 
     def _real_ahead(self, nb):
@@ -652,8 +651,7 @@ class TPGANTrainer:
             self.fD.zero_grad()
             d_real = self.D(tpgan_ops.to_cl(nb["frontal"], self.dtype)).float()
             loss = -d_real.mean()
-            with tpgan_ops.wgrad_side_stream():
-                (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
+            (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
         self._d_real_next = (nb["frontal"], self._real_key(nb["frontal"]), d_real.detach())
 
     def _real_key(self, frontal):
@@ -742,7 +740,7 @@ class TPGANTrainer:
             if self.gsync.optimizer is not None:
                 self.fG.adam_begin(self.betas)  # (the step counter, once, ahead of every bucket's update)
             self.gsync.begin()
-        with tpgan_ops.roctx_range("G-bwd"), tpgan_ops.wgrad_side_stream():
+        with tpgan_ops.roctx_range("G-bwd"):
             (loss_G * self.loss_scale if self.loss_scale != 1.0 else loss_G).backward()
         self._st["loss_G"] = loss_G.detach()
 
