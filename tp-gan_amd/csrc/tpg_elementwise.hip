@@ -95,7 +95,7 @@ __device__ __forceinline__ void pack_halo_block_t(const PackArgs& p, int bn, int
 // first_block), stages the job in LDS and packs TPG_PACK_GROUPS groups of 256 items,
 // ((b - first_block)*TPG_PACK_GROUPS + g)*256 + tid (one group per block measured latency-bound
 // on the search and the job copy: 150 k blocks for G's images).
-__global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restrict__ jobs, int n, int var) {
+__global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restrict__ jobs, int n) {
   __shared__ PackJob job;
   __shared__ int jsel;
   if (threadIdx.x == 0) {
@@ -130,9 +130,9 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restric
     const int idx = (lb0 + g) * 256 + threadIdx.x;
     if (idx >= job.items) break;
     if (job.kind == 1) {
-      if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx, var);
-      else if (job.k.dtype == TPG_F16) pack_halo_item<_Float16>(job.k, job.bn, job.bnl, job.ntiles, idx, var);
-      else pack_halo_item<float>(job.k, job.bn, job.bnl, job.ntiles, idx, var);
+      if (job.k.dtype == TPG_BF16) pack_halo_item<__bf16>(job.k, job.bn, job.bnl, job.ntiles, idx);
+      else if (job.k.dtype == TPG_F16) pack_halo_item<_Float16>(job.k, job.bn, job.bnl, job.ntiles, idx);
+      else pack_halo_item<float>(job.k, job.bn, job.bnl, job.ntiles, idx);
     } else {
       if (job.k.dtype == TPG_BF16) pack_igemm_item<__bf16>(job.k, idx);
       else if (job.k.dtype == TPG_F16) pack_igemm_item<_Float16>(job.k, idx);
@@ -143,8 +143,7 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackJob* __restric
 
 int launch_pack_many(const PackJob* jobs_dev, int n, int nblocks, hipStream_t s) {
   if (n <= 0 || nblocks <= 0) return 0;
-  const char* ev = getenv("TPG_OPT_VAR");  // (temporary A/B switch, tools/bench_opt.py --vars)
-  hipLaunchKernelGGL(pack_many_kernel, dim3(nblocks), dim3(256), 0, s, jobs_dev, n, ev ? atoi(ev) : 0);
+  hipLaunchKernelGGL(pack_many_kernel, dim3(nblocks), dim3(256), 0, s, jobs_dev, n);
   return (int)hipGetLastError();
 }
 

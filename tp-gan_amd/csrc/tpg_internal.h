@@ -323,7 +323,7 @@ __device__ __forceinline__ void pack_igemm_item(const PackArgs& p, int idx) {
 // halo layout: Wp[ks*ntaps + tap][ntile][bnl rows][4 chunks][EPC]; item = one 16-byte chunk;
 // row r of N-tile nt is n' = nt*bn + r, chunk' = chunk ^ hswz(r)
 template <typename E>
-__device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bnl, int ntiles, int idx, int var = 0) {
+__device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bnl, int ntiles, int idx) {
   constexpr int EPC = 16 / sizeof(E);
   constexpr int ROW = 4 * EPC;
   const int pchunk = idx & 3;
@@ -363,9 +363,10 @@ __device__ __forceinline__ void pack_halo_item(const PackArgs& p, int bn, int bn
       const float4 v = reinterpret_cast<const float4*>(src)[q];
       o.e[4 * q] = (E)v.x; o.e[4 * q + 1] = (E)v.y; o.e[4 * q + 2] = (E)v.z; o.e[4 * q + 3] = (E)v.w;
     }
-  } else if (var == 0 && cstride == 1 && row_ok && c0 + EPC <= p.Creal && ((uintptr_t)src % 8) == 0) {
+  } else if (cstride == 1 && row_ok && c0 + EPC <= p.Creal && ((uintptr_t)src % 8) == 0) {
     // (an even channel count that is not a multiple of 4 -- 206 -- leaves every other tap's
-    // rows 8-byte aligned only: 8-byte loads instead of 4-byte ones)
+    // rows 8-byte aligned only: 8-byte loads instead of 4-byte ones; G's re-pack 0.489 ->
+    // 0.470 ms, tools/bench_opt.py, gpurun r06r)
 #pragma unroll
     for (int q = 0; q < EPC / 2; ++q) {
       const float2 v = reinterpret_cast<const float2*>(src)[q];

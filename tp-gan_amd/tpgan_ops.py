@@ -257,11 +257,12 @@ AUTOTUNE = {"enabled": True, "cache": {}, "trials": 0, "frozen": False}
 # (adding the library's own split for each tile, which fills whole rounds of the chip and won
 # several isolated trials, measured 36.22-36.26 vs 36.10-36.14 ms/step in round 3)
 _WG_SPLITS = (1, 2, 4, 8, 16, 32, 64)
-# between the powers of two above 16 (whole-chip shapes only): the 128 x 32 row-halo tile of
-# enhance_128 (70 tiles) fills the chip's 512 resident blocks best at 36 splits -- 1.381 vs
-# 1.405 ms at 32 (tools/bench_layers.py --wg-sweep, gpurun r06n).  False: powers of two (A/B)
-WG_SPLITS_EXTRA = {"enabled": True}
-_WG_SPLITS_X = (1, 2, 4, 8, 16, 24, 32, 36, 48, 64)
+# between the powers of two: the 128 x 32 row-halo tile of enhance_128 (70 tiles) fills the
+# chip's 512 resident blocks best at 36 splits -- 1.381 vs 1.405 ms at 32 (tools/bench_layers.py
+# --wg-sweep, gpurun r06n); 3 / 6 / 12 for the one-round small-map grids (162 tiles x 3 = 1.9
+# rounds of 256 instead of 1.3 at 2).  False: powers of two; "small" False: without 3 / 6 / 12 (A/B)
+WG_SPLITS_EXTRA = {"enabled": True, "small": True}
+_WG_SPLITS_X = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 36, 48, 64)
 
 
 def _desc_tuple(d):
@@ -463,7 +464,8 @@ def _tuned_wgrad(lib, d, x, g, dwv):
     best, best_ms = (0, 0), None
     torch.cuda.synchronize()
     for algo in range(1, 13):
-        for ks in (_WG_SPLITS_X if WG_SPLITS_EXTRA["enabled"] else _WG_SPLITS):
+        for ks in (_WG_SPLITS if not WG_SPLITS_EXTRA["enabled"] else
+                   _WG_SPLITS_X if WG_SPLITS_EXTRA["small"] else tuple(k for k in _WG_SPLITS_X if k not in (3, 6, 12))):
             if ks > nkt or (ks > 16 and (d.flags & FLAG_CONCURRENT)):
                 break
             d.algo, d.ksplit = algo, ks
