@@ -370,12 +370,11 @@ def _time_wgrad(lib, d, x, g, scratch):
 # Measured (profiles/r04/data_split_tuner.txt): configs[1] re-picks 8 of 90 shapes, step unchanged
 # (33.33 vs 33.33 ms interleaved); configs[2]'s ResNet-50 layers gain 38.36 -> 37.93 ms/step.
 _DATA_SPLITS = (0, 1, 2, 4, 8, 16)
-_DATA_SPLITS_X = (0, 1, 2, 3, 4, 6, 8, 12, 16)  # (DATA_TUNE["splits_x"]: also 3 / 6 / 12)
 _DATA_ALGOS = (1, 2)  # desc.data_algo: the halo-tiled kernel, the tap-DMA pointwise kernel
 # log: a list to append (op, shape, {split: ms}, pick) to; margin: a candidate replaces the
 # planner's plan when it takes less than margin x the plan's time (0.97: 30.68 / 30.56 against
 # 30.77 / 31.00 ms/step with round 4's 0.9, alternating bench runs, gpurun r05at)
-DATA_TUNE = {"enabled": True, "log": None, "margin": 0.97, "splits_x": True}
+DATA_TUNE = {"enabled": True, "log": None, "margin": 0.97}
 _DATA_SPLIT_WS_CAP = 256 << 20
 
 
@@ -422,8 +421,7 @@ def _tuned_data_split(lib, d, op, device, launch):
         return (0, 0)
     times = {}
     torch.cuda.synchronize()
-    splits = _DATA_SPLITS_X if DATA_TUNE["splits_x"] else _DATA_SPLITS
-    for cand in [(0, 0)] + [(ks, al) for al in _DATA_ALGOS for ks in splits]:
+    for cand in [(0, 0)] + [(ks, al) for al in _DATA_ALGOS for ks in _DATA_SPLITS]:
         d.data_ksplit, d.data_algo = cand
         if cand[0] > 1 and lib.tpg_conv2d_workspace(ctypes.byref(d), op) > _DATA_SPLIT_WS_CAP:
             continue  # (a split this large never won; its partials would not fit L2 / MALL anyway)
