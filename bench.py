@@ -125,6 +125,9 @@ def parse():
     ap.add_argument("--identity", choices=["none", "resnet50", "mobilenetv2"], default=None,
                     help="identity-preserving loss extractor in the G step (BASELINE configs[2]: resnet50)")
     ap.add_argument("--gp", action="store_true", help="WGAN-GP in the D step (double backward through D)")
+    ap.add_argument("--tune-file", default=None,
+                    help="start from a saved autotuner cache (tpgan_ops.save_tuning / TPG_TUNE_DUMP); shapes "
+                         "it lacks are tuned in the warm-up as usual")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI, the product; gloo: the "
                          "one-GPU rehearsal of this launch path in tests/test_gpu_bench_dp.py)")
@@ -196,6 +199,8 @@ def main():
     # algorithmic FLOPs, then the step is captured as hipGraph(s)
     # (next_b: the next step's batch -- here the same resident one -- so that, data-parallel,
     # its D(real) pass runs under the G all-reduce tail)
+    if args.tune_file:
+        tpgan_ops.load_tuning(args.tune_file)
     for _ in range(max(args.warmup - 1, 0)):
         trainer.step(batch, next_b=batch)
     tpgan_ops.reset_flops()
@@ -366,7 +371,7 @@ def main():
                    "parallelism": "dp%d" % world,
                    "launch": ("eager" + (" (graph capture failed)" if capture_error else "")) if not graphed
                    else ("hipGraph x3 (per phase)" if (world > 1 or args.segmented) else "hipGraph (whole step)"),
-                   "capture_error": capture_error},
+                   "capture_error": capture_error, "tune_file": args.tune_file},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
