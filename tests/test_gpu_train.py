@@ -437,6 +437,42 @@ def test_prepacked_weights_match_inline_packing(gpu):
         assert rel(c[i].cpu(), a[i].cpu()) <= max(3 * floor, 1e-6), (i, rel(c[i].cpu(), a[i].cpu()), floor, diff)
 
 
+def test_prepacked_images_current_after_steps(gpu):
+    """Every pre-packed weight image of G and D equals a fresh pack of the current fp32 weights
+    after eager steps and after graph replays (no entry left out of the batched re-pack, none
+    packed from a stale or foreign weight pointer): each entry's own jobs are re-run and the
+    image must not change, bit for bit."""
+    import tpgan_ops
+    import tpgan_train
+    G, D = _models(gpu)
+    tr = tpgan_train.TPGANTrainer(G, D, compute_dtype=torch.bfloat16, use_dropout=False)
+    b = tpgan_train.synthetic_batch(2, gpu, seed=29)
+    lib = tpgan_ops.load()
+
+    def check_images(tag):
+        torch.cuda.synchronize()
+        n = 0
+        for flat in (tr.fG, tr.fD):
+            for key, e in flat.pack_entries.items():
+                if e is None or not e.njobs:
+                    continue
+                assert e.epoch == flat.epoch, (tag, key[0], key[1][:9], e.epoch, flat.epoch)
+                before = e.buf.clone()
+                tpgan_ops.check(lib.tpg_pack_run(e.dev.data_ptr(), e.njobs, e.nblocks, tpgan_ops.stream_ptr()))
+                torch.cuda.synchronize()
+                assert torch.equal(before, e.buf), (tag, key[0], key[1][:9])
+                n += 1
+        return n
+
+    for _ in range(3):
+        tr.step(b)
+    assert check_images("eager") > 50
+    tr.capture(b, warmup=1)
+    for _ in range(2):
+        tr.step_graphed()
+    assert check_images("graph") > 50
+
+
 def test_deterministic_mode_bit_identical(gpu):
     """tpg_set_deterministic: two bf16 train steps from the same state give bit-identical
     parameters, gradients and Adam moments (SURVEY.md §5 race detection / run-to-run)."""
