@@ -123,4 +123,29 @@ def test_tuning_file_roundtrip_and_old_keys(tmp_path):
         assert tpgan_ops.AUTOTUNE["cache"][kd] == (4, 2)
     finally:
         tpgan_ops.AUTOTUNE["cache"].clear()
+
+
+def test_committed_tuning_caches_load():
+    """The autotuner caches committed under profiles/ (bench.py --tune-file) load: every weight-
+    gradient key has the current field count and every pick is an (algo, split) pair."""
+    import glob
+    import os
+    import tpgan_ops
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                          "profiles", "r06", "tune_*.json")))
+    assert files
+    saved = dict(tpgan_ops.AUTOTUNE["cache"])
+    try:
+        for f in files:
+            tpgan_ops.AUTOTUNE["cache"].clear()
+            tpgan_ops.load_tuning(f)
+            cache = tpgan_ops.AUTOTUNE["cache"]
+            assert len(cache) > 50, f
+            for k, v in cache.items():
+                assert len(v) == 2 and all(isinstance(x, int) for x in v), (f, k, v)
+                if k[0] == "wgrad":
+                    assert len(k[1]) == tpgan_ops._WGRAD_KEY_LEN, (f, k)
+    finally:
+        tpgan_ops.AUTOTUNE["cache"].clear()
+        tpgan_ops.AUTOTUNE["cache"].update(saved)
         tpgan_ops.AUTOTUNE["cache"].update(saved)
